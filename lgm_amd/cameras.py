@@ -1,0 +1,85 @@
+"""Camera construction used by every caller of the renderer.
+
+Restates the recipe of core/provider_lvis.py:200-213 (also infer.py:135-142, gui.py:67-73, convert.py:108-114):
+OpenGL c2w -> flip up/forward columns -> cam_view = inverse(c2w)^T -> cam_view_proj = cam_view @ proj -> cam_pos = -c2w[:3, 3].
+The look-at convention restates kiui.cam.orbit_camera / look_at (EXT, `kiui` is not installed here),
+as called by core/models.py:66-71 and infer.py:135.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+
+def _normalize(v: np.ndarray) -> np.ndarray:
+    return v / max(float(np.linalg.norm(v)), 1e-20)
+
+
+def look_at(campos: np.ndarray, target: np.ndarray, opengl: bool = True) -> np.ndarray:
+    """3x3 camera rotation (columns right, up, forward); kiui.cam.look_at semantics."""
+    up = np.array([0, 1, 0], dtype=np.float32)
+    if not opengl:
+        fwd = _normalize(target - campos)
+        right = _normalize(np.cross(fwd, up))
+        up = _normalize(np.cross(right, fwd))
+    else:
+        fwd = _normalize(campos - target)
+        right = _normalize(np.cross(up, fwd))
+        up = _normalize(np.cross(fwd, right))
+    return np.stack([right, up, fwd], axis=1)
+
+
+def orbit_camera(elevation: float, azimuth: float, radius: float = 1.0, is_degree: bool = True,
+                 target=None, opengl: bool = True) -> np.ndarray:
+    """[4,4] float32 c2w pose on an orbit (kiui.cam.orbit_camera semantics)."""
+    if is_degree:
+        elevation = np.deg2rad(elevation)
+        azimuth = np.deg2rad(azimuth)
+    x = radius * np.cos(elevation) * np.sin(azimuth)
+    y = -radius * np.sin(elevation)
+    z = radius * np.cos(elevation) * np.cos(azimuth)
+    if target is None:
+        target = np.zeros([3], dtype=np.float32)
+    campos = np.array([x, y, z]) + target
+    T = np.eye(4, dtype=np.float32)
+    T[:3, :3] = look_at(campos, target, opengl)
+    T[:3, 3] = campos
+    return T
+
+
+def projection_matrix(fovy: float, znear: float, zfar: float) -> torch.Tensor:
+    """The [4,4] proj of core/gs.py:23-29 / core/provider_lvis.py:59-65 (row-major torch layout)."""
+    tan_half_fov = np.tan(0.5 * np.deg2rad(fovy))
+    P = torch.zeros(4, 4, dtype=torch.float32)
+    P[0, 0] = 1 / tan_half_fov
+    P[1, 1] = 1 / tan_half_fov
+    P[2, 2] = (zfar + znear) / (zfar - znear)
+    P[3, 2] = -(zfar * znear) / (zfar - znear)
+    P[2, 3] = 1
+    return P
+
+
+def cameras_from_c2w(c2w: torch.Tensor, proj: torch.Tensor):
+    """c2w [V,4,4] OpenGL poses -> (cam_view [V,4,4], cam_view_proj [V,4,4], cam_pos [V,3]) per
+    core/provider_lvis.py:200-213."""
+    c2w = c2w.clone().float()
+    c2w[:, :3, 1:3] *= -1
+    cam_view = torch.inverse(c2w).transpose(1, 2)
+    cam_view_proj = cam_view @ proj
+    cam_pos = -c2w[:, :3, 3]
+    return cam_view, cam_view_proj, cam_pos
+
+
+def orbit_cameras(num_views: int, radius: float = 1.5, elevation: float = 0.0, fovy: float = 49.1,
+                  znear: float = 0.5, zfar: float = 2.5, azimuth_offset: float = 0.0):
+    """V evenly spaced orbit cameras (SURVEY.md §8(d) synthetic cameras): returns cam_view, cam_view_proj,
+    cam_pos as [V,4,4], [V,4,4], [V,3] float32 CPU tensors."""
+    poses = np.stack([orbit_camera(elevation, azimuth_offset + 360.0 * v / num_views, radius=radius)
+                      for v in range(num_views)], axis=0)
+    return cameras_from_c2w(torch.from_numpy(poses), projection_matrix(fovy, znear, zfar))
+
+
+def tan_half_fov(fovy: float) -> float:
+    return float(math.tan(0.5 * math.radians(fovy)))

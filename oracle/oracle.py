@@ -1,0 +1,130 @@
+"""ctypes front-end of the CPU rasterizer oracle (oracle/raster_oracle.c) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module. PARITY UNPINNED for
+the rasterizer: see the header of raster_oracle.c. The batched call mirrors core/gs.py:42-93 (B x V loop,
+per-(b, v) rasterizer call on the [N,14] slices, results stacked to [B,V,C,H,W]); the image is returned
+UNCLAMPED (the clamp of core/gs.py:87 is applied by the caller, exactly as the product path applies it in torch).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liblgm_oracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        f32p = ctypes.POINTER(ctypes.c_float)
+        i32p = ctypes.POINTER(ctypes.c_int)
+        i64p = ctypes.POINTER(ctypes.c_longlong)
+        L.lgm_oracle_render_batch.restype = ctypes.c_int
+        L.lgm_oracle_render_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p, f32p, f32p,
+                                              ctypes.c_float, ctypes.c_float, ctypes.c_float, f32p, ctypes.c_int,
+                                              ctypes.c_int, f32p, f32p, f32p, i64p, f32p, f32p, f32p, f32p,
+                                              ctypes.c_int]
+        L.lgm_oracle_render_view.restype = ctypes.c_int
+        L.lgm_oracle_render_view.argtypes = [ctypes.c_int, f32p, f32p, f32p, ctypes.c_float, ctypes.c_float,
+                                             ctypes.c_float, f32p, ctypes.c_int, ctypes.c_int, f32p, f32p, f32p,
+                                             i32p, i64p, f32p, f32p, f32p, f32p, f32p]
+        L.lgm_oracle_preprocess_view.restype = ctypes.c_longlong
+        L.lgm_oracle_preprocess_view.argtypes = [ctypes.c_int, f32p, f32p, f32p, ctypes.c_float, ctypes.c_float,
+                                                 ctypes.c_float, ctypes.c_int, ctypes.c_int, i32p, f32p, f32p,
+                                                 f32p, i32p]
+        L.lgm_oracle_tile_lists.restype = ctypes.c_longlong
+        L.lgm_oracle_tile_lists.argtypes = [ctypes.c_int, f32p, f32p, f32p, ctypes.c_float, ctypes.c_float,
+                                            ctypes.c_float, ctypes.c_int, ctypes.c_int, i32p, i32p, ctypes.c_longlong]
+        _lib = L
+    return _lib
+
+
+def _f(a):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _c(a, dtype=np.float32):
+    return np.ascontiguousarray(np.asarray(a, dtype=dtype))
+
+
+def render(gaussians, cam_view, cam_view_proj, tanfov: float, H: int, W: int, bg, scale_modifier: float = 1.0,
+           d_image=None, d_depth=None, d_alpha=None, nthreads: int = 0):
+    """Forward (+ optional backward) of B x V renders.
+
+    gaussians [B,N,14]; cam_view/cam_view_proj [B,V,4,4] (row-major torch layout, as core/gs.py passes them);
+    bg [3]. Returns dict with image [B,V,3,H,W] (unclamped), depth/alpha [B,V,1,H,W], K (total pairs),
+    evals (pixel-Gaussian evaluations) and, if d_image is given, d_gaussians [B,N,14].
+    """
+    g = _c(gaussians)
+    B, N = g.shape[0], g.shape[1]
+    views = _c(cam_view).reshape(B, -1, 16)
+    V = views.shape[1]
+    projs = _c(cam_view_proj).reshape(B, V, 16)
+    bgv = _c(bg).reshape(3)
+    color = np.zeros((B, V, 3, H, W), np.float32)
+    depth = np.zeros((B, V, 1, H, W), np.float32)
+    alpha = np.zeros((B, V, 1, H, W), np.float32)
+    stats = np.zeros(2, np.int64)
+    dg = None
+    if d_image is not None:
+        d_image = _c(d_image).reshape(B, V, 3, H, W)
+        d_depth = _c(np.zeros((B, V, 1, H, W)) if d_depth is None else d_depth).reshape(B, V, 1, H, W)
+        d_alpha = _c(np.zeros((B, V, 1, H, W)) if d_alpha is None else d_alpha).reshape(B, V, 1, H, W)
+        dg = np.zeros((B, N, 14), np.float32)
+    if nthreads <= 0:
+        nthreads = min(os.cpu_count() or 1, B * V)
+    rc = lib().lgm_oracle_render_batch(B, V, N, _f(g), _f(views), _f(projs), float(tanfov), float(tanfov),
+                                       float(scale_modifier), _f(bgv), H, W, _f(color), _f(depth), _f(alpha),
+                                       stats.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), _f(d_image),
+                                       _f(d_depth), _f(d_alpha), _f(dg), int(nthreads))
+    if rc != 0:
+        raise RuntimeError("oracle render failed")
+    out = {"image": color, "depth": depth, "alpha": alpha, "K": int(stats[0]), "evals": int(stats[1])}
+    if dg is not None:
+        out["d_gaussians"] = dg
+    return out
+
+
+def preprocess(g_scene, view16, proj16, tanfov: float, H: int, W: int, scale_modifier: float = 1.0):
+    """Per-Gaussian records of one view: radii, xy, depth, conic_opacity, rect, K."""
+    g = _c(g_scene)
+    N = g.shape[0]
+    radii = np.zeros(N, np.int32)
+    xy = np.zeros((N, 2), np.float32)
+    depth = np.zeros(N, np.float32)
+    conic = np.zeros((N, 4), np.float32)
+    rect = np.zeros((N, 4), np.int32)
+    i32 = ctypes.POINTER(ctypes.c_int)
+    K = lib().lgm_oracle_preprocess_view(N, _f(g), _f(_c(view16).reshape(16)), _f(_c(proj16).reshape(16)),
+                                         float(tanfov), float(tanfov), float(scale_modifier), H, W,
+                                         radii.ctypes.data_as(i32), _f(xy), _f(depth), _f(conic),
+                                         rect.ctypes.data_as(i32))
+    return {"radii": radii, "xy": xy, "depth": depth, "conic_opacity": conic, "rect": rect, "K": int(K)}
+
+
+def tile_lists(g_scene, view16, proj16, tanfov: float, H: int, W: int, scale_modifier: float = 1.0):
+    """Sorted per-tile Gaussian lists of one view: (tile_start [T+1], ids [K])."""
+    g = _c(g_scene)
+    N = g.shape[0]
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    ts = np.zeros(T + 1, np.int32)
+    i32 = ctypes.POINTER(ctypes.c_int)
+    args = (N, _f(g), _f(_c(view16).reshape(16)), _f(_c(proj16).reshape(16)), float(tanfov), float(tanfov),
+            float(scale_modifier), H, W, ts.ctypes.data_as(i32))
+    K = lib().lgm_oracle_tile_lists(*args, None, 0)
+    ids = np.zeros(max(K, 1), np.int32)
+    lib().lgm_oracle_tile_lists(*args, ids.ctypes.data_as(i32), K)
+    return ts, ids[:K]

@@ -1,0 +1,170 @@
+"""bench.py -- BASELINE.json metric: Mpixels/s of forward+backward Gaussian rasterization, 256^2, 100k Gaussians,
+6 views (BASELINE config 3), on 1/2/4/8 MI355X.
+
+A step = GaussianRenderer.render (core/gs.py:31-98 API: forward of all 6 views, clamp) + autograd backward to
+dL/dgaussians [1,N,14] for fixed seeded upstream gradients. Weak scaling: every rank renders its OWN scene
+(seed 1 + rank; scene-sharded, no data-path collective); value = total pixels of all ranks / max
+rank time. Per-kernel durations come from HIP events recorded by liblgm_amd on the launch stream inside the timed
+region (lgm_amd._native.KernelProfiler); `roofline` prices the dominant kernel with SURVEY.md §8(d)'s algorithmic
+bytes. The CPU baseline (rank 0, N=1) is the oracle port (oracle/raster_oracle.c, OpenMP over views) on the same
+scene for a bounded number of repetitions.
+
+    python bench.py [--gpus N --steps K --warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+N_GAUSS, VIEWS, RES = 100_000, 6, 256
+
+
+def kernel_bytes(N, V, K, P):
+    """SURVEY.md §8(d) algorithmic bytes per launch (all V views of one scene): fwd = 56N + 60K + 20P,
+    bwd = 112N + 84K + 28P per view; K is summed over views here."""
+    return {
+        "k_preprocess": 56 * N * V,
+        "k_emit": 8 * K,
+        "k_sort": 8 * K,
+        "k_render_fwd": 44 * K + 20 * P * V,
+        "k_render_bwd": 84 * K + 28 * P * V,
+        "k_preproc_bwd": 112 * N * V,
+    }
+
+
+def cpu_baseline(g, cv, cvp, tan, bg, d_img, d_alpha, seconds):
+    from oracle import oracle as O
+    O.build()
+    threads = min(os.cpu_count() or 1, VIEWS)
+    args = (g.numpy(), cv.numpy(), cvp.numpy(), tan, RES, RES, bg.numpy())
+    kw = dict(d_image=d_img.numpy(), d_alpha=d_alpha.numpy(), nthreads=threads)
+    O.render(*args, **kw)  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        O.render(*args, **kw)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(reps * VIEWS * RES * RES / el / 1e6, 3), "unit": "Mpixels/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle/raster_oracle.c fwd+bwd of the rank-0 cfg3 scene (100k Gaussians x 6 views x 256^2), "
+                      f"{reps} repetitions in {el:.1f} s, OpenMP over views"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from lgm_amd import GaussianRenderer, Options, _native
+    from lgm_amd.cameras import orbit_cameras
+    from lgm_amd.gs import count_pairs
+    from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads
+
+    seed = 1 + rank
+    g_cpu = synthetic_gaussians(1, N_GAUSS, seed=seed)
+    cv, cvp, cp = orbit_cameras(VIEWS)
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(1, VIEWS, RES, RES, seed=seed + 1000)
+    renderer = GaussianRenderer(Options(output_size=RES))
+    g = g_cpu.to(dev).requires_grad_(True)
+    cvd, cvpd, cpd = cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev)
+    bgd, d_imgd, d_alphad = bg.to(dev), d_img.to(dev), d_alpha.to(dev)
+    tan = float(renderer.tan_half_fov)
+    K = count_pairs(g.detach(), cvd, cvpd, tan, tan, RES, RES)
+
+    def step():
+        out = renderer.render(g, cvd, cvpd, cpd, bg_color=bgd)
+        torch.autograd.backward([out["image"], out["alpha"]], [d_imgd, d_alphad])
+        g.grad = None
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    prof = _native.KernelProfiler()
+    barrier()
+    torch.cuda.synchronize()
+    with prof:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+    kern = prof.summary()
+    prof.close()
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+
+    P = RES * RES
+    pixels = world * VIEWS * P * args.steps
+    value = pixels / el / 1e6
+    kb = kernel_bytes(N_GAUSS, VIEWS, K, P)
+    per_kernel = {k: {"avg_us": round(1e3 * ms / n, 2), "launches": n} for k, (n, ms) in kern.items()}
+    dom = max(kern.items(), key=lambda kv: kv[1][1])[0]
+    dom_avg_s = kern[dom][1] / kern[dom][0] / 1e3
+    achieved = kb.get(dom, 0) / dom_avg_s / 1e9
+    step_bytes = sum(kb.values())
+    ms_step = 1e3 * el / args.steps
+    result = {
+        "metric": "Mpixels/s fwd+bwd Gaussian raster (256^2, 100k gauss, 6 views)",
+        "value": round(value, 2),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SURVEY.md 8(d): raw~N(0,1) through LGM activations, 6 orbit cameras r=1.5 fovy 49.1, "
+                "seeded upstream grads); one scene per GPU",
+        "config": {"workload": "cfg3: 100k Gaussians x 6 views x 256^2, render fwd+bwd (GaussianRenderer API)",
+                   "gaussians": N_GAUSS, "views": VIEWS, "H": RES, "W": RES, "scenes_per_gpu": 1,
+                   "pairs_K_per_scene": K, "parallelism": f"scene-sharded x{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                     "bytes_per_launch": kb.get(dom, 0)},
+        "step_roofline": {"bytes": step_bytes, "achieved_GBs": round(step_bytes / (ms_step / 1e3) / 1e9, 2),
+                          "frac": round(step_bytes / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4)},
+        "kernels": per_kernel,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(g_cpu, cv[None], cvp[None], tan, bg, d_img, d_alpha,
+                                              args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

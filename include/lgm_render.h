@@ -1,0 +1,71 @@
+/*
+ * lgm_render.h -- C ABI of the MI355X-native Gaussian-splat render path (liblgm_amd.so).
+ *
+ * Replaces the external CUDA extension `diff_gaussian_rasterization._C` that LGM reaches through
+ * core/gs.py:7-10 and calls once per (scene b, view v) at core/gs.py:58-85:
+ *   - lgm_render_forward  replaces _C.rasterize_gaussians          (the per-view forward behind
+ *                         GaussianRasterizer(...)(...) at core/gs.py:73-85), batched over all B x V views;
+ *   - lgm_render_backward replaces _C.rasterize_gaussians_backward (driven by autograd from main.py:102
+ *                         through the EXT autograd Function), batched likewise, and additionally performs the
+ *                         sum over views + slice-gradient scatter that autograd does through the slices of
+ *                         core/gs.py:45-49, writing dL/dgaussians [B,N,14] directly.
+ * The Python side (lgm_amd/gs.py) keeps the reference's GaussianRenderer API (core/gs.py:16-98).
+ *
+ * Conventions (all pointers are DEVICE pointers unless stated; all arrays dense, row-major, fp32):
+ *   gaussians      [B,N,14]  pos(3) opacity(1) scale(3) rotation(4: w,x,y,z) rgb(3)   (core/gs.py:45-49)
+ *   cam_view       [B,V,4,4] the transposed w2c exactly as core/gs.py:54 passes it (read column-major)
+ *   cam_view_proj  [B,V,4,4] likewise (core/gs.py:55)
+ *   bg             [3]
+ *   image          [B,V,3,H,W] UNCLAMPED (core/gs.py:87's clamp is applied by the caller, as the reference does)
+ *   depth, alpha   [B,V,1,H,W]
+ * Error behaviour: every entry point returns 0 on success and a negative LGM_E* code on failure; it never
+ * throws across the ABI. lgm_last_error() returns a thread-local description of the last failure.
+ * Threading: stream-ordered (all work is enqueued on `stream`, a hipStream_t passed as void*), no host
+ * synchronisation inside forward/backward, reentrant; no global mutable state other than the error string.
+ * Memory: caller-owned. Scratch and saved-for-backward state live in ONE caller-allocated workspace whose size
+ * is given by lgm_render_workspace_size(); the same workspace must be passed, untouched, to the backward.
+ */
+#ifndef LGM_RENDER_H
+#define LGM_RENDER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "lgm_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Workspace bytes for B x V renders of N Gaussians at H x W with room for `pair_capacity` (Gaussian, tile)
+ * pairs in total over all views. pair_capacity <= 0 selects the worst case B*V*N*tiles (never overflows). */
+size_t lgm_render_workspace_size(int B, int V, int N, int H, int W, long long pair_capacity);
+
+/* Exact number of (Gaussian, tile) pairs K over all B x V views (the reference's `num_rendered`, summed).
+ * Enqueues a counting pass and writes K to *pairs_out (a DEVICE int64). Used by callers that cannot afford the
+ * worst-case workspace; they synchronise once, size the workspace from K and then call lgm_render_forward. */
+int lgm_render_count_pairs(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                           const float *cam_view_proj, float tanfovx, float tanfovy, float scale_modifier,
+                           void *workspace, size_t workspace_bytes, long long *pairs_out, void *stream);
+
+/* Forward of all B x V renders (replaces B*V calls of _C.rasterize_gaussians). radii_out [B,V,N] int32 may be
+ * NULL. stats_out, if not NULL, is a DEVICE int64[2]: {K = total pairs, overflow flag}. */
+int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                       const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
+                       float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
+                       void *workspace, size_t workspace_bytes, long long pair_capacity, long long *stats_out,
+                       void *stream);
+
+/* Backward of all B x V renders (replaces B*V calls of _C.rasterize_gaussians_backward plus the autograd sum
+ * over views). d_depth / d_alpha may be NULL (treated as zero). Writes d_gaussians [B,N,14] (overwrites).
+ * d_means2D [B,V,N,2] (screen-space gradients, what upstream returns for means2D) may be NULL. */
+int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                        const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
+                        float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
+                        float *d_gaussians, float *d_means2D, void *workspace, size_t workspace_bytes,
+                        long long pair_capacity, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,111 @@
+"""ctypes binding of the C ABI in include/lgm_render.h and include/lgm_attn.h (liblgm_amd.so).
+
+There is no fallback: if the library is missing or cannot be loaded, every op raises. torch is imported first so
+that the library's NEEDED libamdhip64.so.7 resolves to the HIP runtime torch already loaded (same soname), giving
+one HIP runtime per process and letting device pointers and streams flow between torch and the library.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see above)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "liblgm_amd.so")
+
+_c_int, _c_ll, _c_float, _c_size, _vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+
+SIGNATURES = {
+    "lgm_abi_version": (_c_int, []),
+    "lgm_last_error": (ctypes.c_char_p, []),
+    "lgm_render_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_ll]),
+    "lgm_render_count_pairs": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_float, _c_float,
+                                        _c_float, _vp, _c_size, _vp, _vp]),
+    "lgm_render_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_float,
+                                    _c_float, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _vp, _vp]),
+    "lgm_render_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_float,
+                                     _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _vp]),
+    "lgm_attn_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp, _vp, _vp, _c_size, _vp]),
+    "lgm_attn_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "lgm_profiler_create": (_vp, []),
+    "lgm_profiler_attach": (_c_int, [_vp]),
+    "lgm_profiler_summary": (_c_int, [_vp, ctypes.c_char_p, _c_size]),
+    "lgm_profiler_reset": (_c_int, [_vp]),
+    "lgm_profiler_destroy": (None, [_vp]),
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"lgm_amd native library not built ({LIB_PATH}); run `python -m lgm_amd.build`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().lgm_last_error()
+        raise NativeError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device_tensor(t: torch.Tensor, name: str):
+    if not t.is_cuda:
+        raise NativeError(f"{name} must be a GPU tensor: lgm_amd has no CPU path (the reference's rasterizer is "
+                          "GPU-only too, core/gs.py:20)")
+
+
+class KernelProfiler:
+    """HIP events around every kernel liblgm_amd launches from this thread, on the launching stream
+    (include/lgm_common.h). summary() -> {kernel: (launches, total_ms)}."""
+
+    def __init__(self):
+        self.h = lib().lgm_profiler_create()
+
+    def __enter__(self):
+        lib().lgm_profiler_attach(self.h)
+        return self
+
+    def __exit__(self, *exc):
+        lib().lgm_profiler_attach(None)
+
+    def reset(self):
+        lib().lgm_profiler_reset(self.h)
+
+    def summary(self):
+        buf = ctypes.create_string_buffer(1 << 16)
+        check(lib().lgm_profiler_summary(self.h, buf, len(buf)), "lgm_profiler_summary")
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, n, ms = line.split()
+            out[name] = (int(n), float(ms))
+        return out
+
+    def close(self):
+        if self.h:
+            lib().lgm_profiler_destroy(self.h)
+            self.h = None

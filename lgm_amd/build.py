@@ -1,0 +1,49 @@
+"""Builds the in-tree HIP library lgm_amd/_lib/liblgm_amd.so for gfx950 with hipcc (no JIT cache, no torch
+C++ ABI: the library exports a plain C ABI, include/*.h). Run: python -m lgm_amd.build"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SOURCES = ["csrc/common.hip", "csrc/render.hip", "csrc/attention.hip"]
+OUT = os.path.join(HERE, "_lib", "liblgm_amd.so")
+ARCH = os.environ.get("LGM_AMD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def sources():
+    return [os.path.join(HERE, s) for s in SOURCES if os.path.exists(os.path.join(HERE, s))]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = sources() + [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
+    return any(os.path.getmtime(p) > t for p in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    objs = []
+    for src in sources():
+        obj = os.path.join(HERE, "_lib", os.path.basename(src) + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+               "-munsafe-fp-atomics", "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = OUT + ".tmp"
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,109 @@
+// lgm_amd/csrc/common.hip -- error string + thread-local HIP-event profiler (include/lgm_common.h).
+#include "common.h"
+
+#include <stdarg.h>
+#include <string.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "lgm_common.h"
+
+struct lgm_profiler {
+    struct Rec { const char *name; hipEvent_t a, b; };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+};
+
+namespace lgm {
+static thread_local char g_err[512] = {0};
+static thread_local lgm_profiler *g_prof = nullptr;
+static thread_local const char *g_pending = nullptr;
+static thread_local hipEvent_t g_pending_ev = nullptr;
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+void clear_error() { g_err[0] = 0; }
+
+void prof_begin(const char *name, hipStream_t st) {
+    if (!g_prof) return;
+    g_pending = name;
+    g_pending_ev = g_prof->get();
+    if (g_pending_ev) hipEventRecord(g_pending_ev, st);
+}
+void prof_end(hipStream_t st) {
+    if (!g_prof || !g_pending_ev) return;
+    hipEvent_t b = g_prof->get();
+    if (!b) return;
+    (void)hipEventRecord(b, st);
+    g_prof->recs.push_back({g_pending, g_pending_ev, b});
+    g_pending_ev = nullptr;
+}
+}  // namespace lgm
+
+extern "C" {
+const char *lgm_last_error(void) { return lgm::g_err; }
+int lgm_abi_version(void) { return 1; }
+
+lgm_profiler *lgm_profiler_create(void) { return new lgm_profiler(); }
+int lgm_profiler_attach(lgm_profiler *p) {
+    lgm::g_prof = p;
+    return LGM_OK;
+}
+int lgm_profiler_reset(lgm_profiler *p) {
+    if (!p) return LGM_E_INVALID;
+    p->recs.clear();
+    p->used = 0;
+    return LGM_OK;
+}
+int lgm_profiler_summary(lgm_profiler *p, char *buf, size_t len) {
+    if (!p || !buf || len == 0) return LGM_E_INVALID;
+    std::map<std::string, std::pair<int, double>> agg;
+    std::vector<std::string> order;
+    for (auto &r : p->recs) {
+        if (hipEventSynchronize(r.b) != hipSuccess) {
+            lgm::set_error("event sync failed");
+            return LGM_E_HIP;
+        }
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, r.a, r.b);
+        auto it = agg.find(r.name);
+        if (it == agg.end()) {
+            order.push_back(r.name);
+            agg[r.name] = {1, ms};
+        } else {
+            it->second.first++;
+            it->second.second += ms;
+        }
+    }
+    std::string out;
+    char line[256];
+    for (auto &n : order) {
+        snprintf(line, sizeof(line), "%s %d %.6f\n", n.c_str(), agg[n].first, agg[n].second);
+        out += line;
+    }
+    strncpy(buf, out.c_str(), len - 1);
+    buf[len - 1] = 0;
+    return LGM_OK;
+}
+void lgm_profiler_destroy(lgm_profiler *p) {
+    if (!p) return;
+    if (lgm::g_prof == p) lgm::g_prof = nullptr;
+    for (auto e : p->pool) (void)hipEventDestroy(e);
+    delete p;
+}
+}

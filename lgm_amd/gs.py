@@ -1,0 +1,185 @@
+"""Drop-in GaussianRenderer (core/gs.py:16-190) on the MI355X-native render path.
+
+Same constructor (reads opt.fovy/znear/zfar at construction like core/gs.py:19-29 and opt.output_size at EVERY
+render call like core/gs.py:59-60,92-93, because convert.py:188,265,366 mutate it), same `render` signature and
+returned keys ("image" clamped to [0,1] as core/gs.py:87, "alpha"), plus an additive "depth" key, and the same
+save_ply / load_ply. The B x V python loop of core/gs.py:42-90 and its B*V per-view extension calls (each with a
+device->host sync) are replaced by ONE batched C-ABI call (include/lgm_render.h) per forward and per backward.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+
+from . import _native
+from .ply import read_ply, write_ply
+
+# Sync-free worst-case workspace when it fits this many bytes; otherwise count pairs exactly (one host sync).
+_WS_BUDGET = int(float(os.environ.get("LGM_AMD_WS_BUDGET_GB", "8")) * (1 << 30))
+
+
+def _tiles(H: int, W: int) -> int:
+    return ((W + 15) // 16) * ((H + 15) // 16)
+
+
+class _RasterizeBatched(torch.autograd.Function):
+    """Autograd Function over all B x V renders (replaces B*V applications of the EXT _RasterizeGaussians)."""
+
+    @staticmethod
+    def forward(ctx, g, cam_view, cam_view_proj, bg, tanx, tany, scale_modifier, H, W):
+        L = _native.lib()
+        B, N = g.shape[0], g.shape[1]
+        V = cam_view.shape[1]
+        dev = g.device
+        stream = _native.stream_of(dev)
+        worst = B * V * N * _tiles(H, W)
+        cap = 0
+        ws_bytes = L.lgm_render_workspace_size(B, V, N, H, W, 0)
+        if ws_bytes > _WS_BUDGET or worst >= 2 ** 31:
+            # exact pair count (the reference syncs once per view for this; we sync once per batch)
+            small = L.lgm_render_workspace_size(B, V, N, H, W, 1)
+            ws = torch.empty(small, dtype=torch.uint8, device=dev)
+            k = torch.zeros(2, dtype=torch.int64, device=dev)
+            _native.check(L.lgm_render_count_pairs(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
+                                                   _native.ptr(cam_view_proj), tanx, tany, scale_modifier,
+                                                   _native.ptr(ws), small, _native.ptr(k), stream),
+                          "lgm_render_count_pairs")
+            cap = max(int(k[0].item()), 1)
+            ws_bytes = L.lgm_render_workspace_size(B, V, N, H, W, cap)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        image = torch.empty(B, V, 3, H, W, dtype=torch.float32, device=dev)
+        depth = torch.empty(B, V, 1, H, W, dtype=torch.float32, device=dev)
+        alpha = torch.empty(B, V, 1, H, W, dtype=torch.float32, device=dev)
+        _native.check(L.lgm_render_forward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
+                                           _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
+                                           _native.ptr(image), _native.ptr(depth), _native.ptr(alpha), None,
+                                           _native.ptr(ws), ws_bytes, cap, None, stream), "lgm_render_forward")
+        ctx.save_for_backward(g, cam_view, cam_view_proj, bg)
+        ctx.ws, ctx.ws_bytes, ctx.cap = ws, ws_bytes, cap
+        ctx.params = (tanx, tany, scale_modifier, H, W)
+        return image, depth, alpha
+
+    @staticmethod
+    def backward(ctx, d_image, d_depth, d_alpha):
+        g, cam_view, cam_view_proj, bg = ctx.saved_tensors
+        tanx, tany, scale_modifier, H, W = ctx.params
+        B, N = g.shape[0], g.shape[1]
+        V = cam_view.shape[1]
+        if d_image is None:
+            d_image = torch.zeros(B, V, 3, H, W, dtype=torch.float32, device=g.device)
+        d_image = d_image.float().contiguous()
+        d_depth = None if d_depth is None else d_depth.float().contiguous()
+        d_alpha = None if d_alpha is None else d_alpha.float().contiguous()
+        d_g = torch.empty_like(g)
+        L = _native.lib()
+        _native.check(L.lgm_render_backward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
+                                            _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
+                                            _native.ptr(d_image), _native.ptr(d_depth), _native.ptr(d_alpha),
+                                            _native.ptr(d_g), None, _native.ptr(ctx.ws), ctx.ws_bytes, ctx.cap,
+                                            _native.stream_of(g.device)), "lgm_render_backward")
+        return d_g, None, None, None, None, None, None, None, None
+
+
+def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, scale_modifier=1.0):
+    """Functional form: returns (image [B,V,3,H,W] UNCLAMPED, depth [B,V,1,H,W], alpha [B,V,1,H,W])."""
+    for t, n in ((gaussians, "gaussians"), (cam_view, "cam_view"), (cam_view_proj, "cam_view_proj")):
+        _native.require_device_tensor(t, n)
+    g = gaussians.float().contiguous()
+    dev = g.device
+    cv = cam_view.to(dev, torch.float32).contiguous()
+    cvp = cam_view_proj.to(dev, torch.float32).contiguous()
+    bgt = torch.as_tensor(bg, dtype=torch.float32).to(dev).contiguous().detach()
+    if g.dim() != 3 or g.shape[-1] != 14:
+        raise ValueError(f"gaussians must be [B,N,14], got {tuple(g.shape)}")
+    if cv.shape[:2] != cvp.shape[:2] or cv.shape[0] != g.shape[0] or cv.shape[-2:] != (4, 4):
+        raise ValueError("cam_view / cam_view_proj must be [B,V,4,4] with B matching gaussians")
+    return _RasterizeBatched.apply(g, cv, cvp, bgt, float(tanfovx), float(tanfovy), float(scale_modifier),
+                                   int(H), int(W))
+
+
+def count_pairs(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scale_modifier=1.0) -> int:
+    """Exact total (Gaussian, tile) pair count K over all B x V views -- the reference's `num_rendered` summed
+    over views (one host sync). Used for byte accounting in bench.py."""
+    L = _native.lib()
+    g = gaussians.float().contiguous()
+    B, N, V = g.shape[0], g.shape[1], cam_view.shape[1]
+    dev = g.device
+    small = L.lgm_render_workspace_size(B, V, N, H, W, 1)
+    ws = torch.empty(small, dtype=torch.uint8, device=dev)
+    k = torch.zeros(2, dtype=torch.int64, device=dev)
+    cv = cam_view.to(dev, torch.float32).contiguous()
+    cvp = cam_view_proj.to(dev, torch.float32).contiguous()
+    _native.check(L.lgm_render_count_pairs(B, V, N, H, W, _native.ptr(g), _native.ptr(cv), _native.ptr(cvp),
+                                           float(tanfovx), float(tanfovy), float(scale_modifier), _native.ptr(ws),
+                                           small, _native.ptr(k), _native.stream_of(dev)), "lgm_render_count_pairs")
+    return int(k[0].item())
+
+
+class GaussianRenderer:
+    """core/gs.py:16 GaussianRenderer, same API."""
+
+    def __init__(self, opt):
+        self.opt = opt
+        # core/gs.py:20 creates this on "cuda"; here it follows the Gaussians' device at render time.
+        self.bg_color = torch.tensor([1, 1, 1], dtype=torch.float32,
+                                     device="cuda" if torch.cuda.is_available() else "cpu")
+        self.tan_half_fov = np.tan(0.5 * np.deg2rad(self.opt.fovy))
+        self.proj_matrix = torch.zeros(4, 4, dtype=torch.float32)
+        self.proj_matrix[0, 0] = 1 / self.tan_half_fov
+        self.proj_matrix[1, 1] = 1 / self.tan_half_fov
+        self.proj_matrix[2, 2] = (opt.zfar + opt.znear) / (opt.zfar - opt.znear)
+        self.proj_matrix[3, 2] = -(opt.zfar * opt.znear) / (opt.zfar - opt.znear)
+        self.proj_matrix[2, 3] = 1
+
+    def render(self, gaussians, cam_view, cam_view_proj, cam_pos, bg_color=None, scale_modifier=1):
+        # gaussians [B,N,14]; cam_view, cam_view_proj [B,V,4,4]; cam_pos [B,V,3] (unused without SH, as upstream)
+        S = int(self.opt.output_size)
+        bg = self.bg_color if bg_color is None else bg_color
+        tan = float(self.tan_half_fov)
+        image, depth, alpha = rasterize(gaussians, cam_view, cam_view_proj, bg, tan, tan, S, S, scale_modifier)
+        image = image.clamp(0, 1)  # core/gs.py:87
+        return {"image": image, "alpha": alpha, "depth": depth}
+
+    def save_ply(self, gaussians, path, compatible=True):
+        """core/gs.py:101-152: B == 1, prune opacity < 0.005, optionally invert activations (3DGS PLY layout)."""
+        assert gaussians.shape[0] == 1, "only support batch size 1"
+        g = gaussians[0].detach().float().cpu()
+        means3D, opacity, scales, rotations = g[:, 0:3], g[:, 3:4], g[:, 4:7], g[:, 7:11]
+        shs = g[:, 11:].unsqueeze(1)
+        mask = opacity.squeeze(-1) >= 0.005
+        means3D, opacity, scales, rotations, shs = means3D[mask], opacity[mask], scales[mask], rotations[mask], shs[mask]
+        if compatible:
+            o = opacity.clamp(1e-6, 1 - 1e-6)
+            opacity = torch.log(o / (1 - o))  # kiui.op.inverse_sigmoid
+            scales = torch.log(scales + 1e-8)
+            shs = (shs - 0.5) / 0.28209479177387814
+        f_dc = shs.transpose(1, 2).flatten(start_dim=1).contiguous()
+        names = ["x", "y", "z"] + [f"f_dc_{i}" for i in range(f_dc.shape[1])] + ["opacity"] + \
+                [f"scale_{i}" for i in range(scales.shape[1])] + [f"rot_{i}" for i in range(rotations.shape[1])]
+        data = torch.cat([means3D, f_dc, opacity, scales, rotations], dim=1).numpy().astype(np.float32)
+        write_ply(path, names, data)
+
+    def load_ply(self, path, compatible=True):
+        """core/gs.py:154-190: returns a CPU [N,14] tensor."""
+        props = read_ply(path)
+        xyz = np.stack([props["x"], props["y"], props["z"]], axis=1)
+        print("Number of points at loading : ", xyz.shape[0])
+        opac = props["opacity"][:, None]
+        shs = np.stack([props["f_dc_0"], props["f_dc_1"], props["f_dc_2"]], axis=1)
+        sn = sorted([k for k in props if k.startswith("scale_")], key=lambda s: int(s.split("_")[-1]))
+        rn = sorted([k for k in props if k.startswith("rot_")], key=lambda s: int(s.split("_")[-1]))
+        scales = np.stack([props[k] for k in sn], axis=1)
+        rots = np.stack([props[k] for k in rn], axis=1)
+        gaussians = torch.from_numpy(np.concatenate([xyz, opac, scales, rots, shs], axis=1).astype(np.float64)).float()
+        if compatible:
+            gaussians[..., 3:4] = torch.sigmoid(gaussians[..., 3:4])
+            gaussians[..., 4:7] = torch.exp(gaussians[..., 4:7])
+            gaussians[..., 11:] = 0.28209479177387814 * gaussians[..., 11:] + 0.5
+        return gaussians
+
+
+def tan_half_fov(fovy: float) -> float:
+    return math.tan(0.5 * math.radians(fovy))

@@ -1,0 +1,39 @@
+"""Shared scene builders for render tests (CPU-side inputs, seeded)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from lgm_amd.cameras import orbit_cameras, tan_half_fov
+from lgm_amd.synthetic import synthetic_gaussians
+
+TAN = tan_half_fov(49.1)
+
+
+def scene(B=1, N=1000, V=2, seed=0, shrink=1.0, scale_mul=1.0, elevation=0.0, az_offset=0.0, max_opacity=None):
+    g = synthetic_gaussians(B, N, seed=seed)
+    g[..., 0:3] *= shrink
+    g[..., 4:7] *= scale_mul
+    if max_opacity is not None:
+        g[..., 3] = g[..., 3].clamp(max=max_opacity)
+    cvs, cvps = [], []
+    for b in range(B):
+        cv, cvp, _ = orbit_cameras(V, elevation=elevation, azimuth_offset=az_offset + 17.0 * b)
+        cvs.append(cv)
+        cvps.append(cvp)
+    return g, torch.stack(cvs), torch.stack(cvps)
+
+
+def upstream(B, V, H, W, seed=7):
+    gen = torch.Generator().manual_seed(seed)
+    d_img = torch.randn(B, V, 3, H, W, generator=gen)
+    d_depth = torch.randn(B, V, 1, H, W, generator=gen)
+    d_alpha = torch.randn(B, V, 1, H, W, generator=gen)
+    bg = torch.rand(3, generator=gen)
+    return d_img, d_depth, d_alpha, bg
+
+
+def rel_l2(a, b) -> float:
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))

@@ -28,10 +28,11 @@ N_GAUSS, VIEWS, RES = 100_000, 6, 256
 
 def kernel_bytes(N, V, K, P):
     """SURVEY.md §8(d) algorithmic bytes per launch (all V views of one scene): fwd = 56N + 60K + 20P,
-    bwd = 112N + 84K + 28P per view; K is summed over views here."""
+    bwd = 112N + 84K + 28P per view, K = upstream's num_rendered (summed over views here) even though fewer pairs
+    are binned after exact culling (a build that culls more is still credited with K_ref).
+    k_bin (preprocess + emit) carries 56N + 8K per view, k_sort 8K."""
     return {
-        "k_preprocess": 56 * N * V,
-        "k_emit": 8 * K,
+        "k_bin": 56 * N * V + 8 * K,
         "k_sort": 8 * K,
         "k_render_fwd": 44 * K + 20 * P * V,
         "k_render_bwd": 84 * K + 28 * P * V,
@@ -93,7 +94,7 @@ def main():
     cvd, cvpd, cpd = cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev)
     bgd, d_imgd, d_alphad = bg.to(dev), d_img.to(dev), d_alpha.to(dev)
     tan = float(renderer.tan_half_fov)
-    K = count_pairs(g.detach(), cvd, cvpd, tan, tan, RES, RES)
+    K_binned, K = count_pairs(g.detach(), cvd, cvpd, tan, tan, RES, RES)
 
     def step():
         out = renderer.render(g, cvd, cvpd, cpd, bg_color=bgd)
@@ -149,7 +150,7 @@ def main():
                 "seeded upstream grads); one scene per GPU",
         "config": {"workload": "cfg3: 100k Gaussians x 6 views x 256^2, render fwd+bwd (GaussianRenderer API)",
                    "gaussians": N_GAUSS, "views": VIEWS, "H": RES, "W": RES, "scenes_per_gpu": 1,
-                   "pairs_K_per_scene": K, "parallelism": f"scene-sharded x{world}"},
+                   "pairs_K_reference": K, "pairs_binned": K_binned, "parallelism": f"scene-sharded x{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
                      "bytes_per_launch": kb.get(dom, 0)},

@@ -1,6 +1,6 @@
 /*
  * lgm_common.h -- C ABI shared by the render and attention entry points of liblgm_amd.so:
- * error reporting and an optional per-thread kernel profiler (HIP events recorded on the caller's stream around
+ * error reporting and an optional kernel profiler (HIP events recorded on the caller's stream around
  * every kernel the library launches). There is no reference counterpart: the reference has no profiling hooks
  * beyond the CUDA-event FPS label of gui.py:59-104; bench.py uses this to time the dominant
  * kernel live inside the timed region.
@@ -23,7 +23,8 @@ const char *lgm_last_error(void);
 /* ABI version (bumped on any signature change). */
 int lgm_abi_version(void);
 
-/* Profiler: create, attach to the calling thread (NULL detaches), read per-kernel totals, destroy.
+/* Profiler: create, attach process-wide (NULL detaches; the only mutable global besides the per-thread error
+ * string), read per-kernel totals, destroy.
  * lgm_profiler_summary synchronises on the recorded events and writes lines "name count total_ms\n". */
 typedef struct lgm_profiler lgm_profiler;
 lgm_profiler *lgm_profiler_create(void);

@@ -37,19 +37,22 @@
 extern "C" {
 #endif
 
-/* Workspace bytes for B x V renders of N Gaussians at H x W with room for `pair_capacity` (Gaussian, tile)
- * pairs in total over all views. pair_capacity <= 0 selects the worst case B*V*N*tiles (never overflows). */
+/* Workspace bytes for B x V renders of N Gaussians at H x W. pair_capacity <= 0 selects SLOT mode: every tile owns
+ * room for N pairs (B*V*N*tiles*8 bytes, no counting pass, no host sync). pair_capacity > 0 selects PACKED mode
+ * with room for that many (Gaussian, tile) pairs in total (from lgm_render_count_pairs). */
 size_t lgm_render_workspace_size(int B, int V, int N, int H, int W, long long pair_capacity);
 
-/* Exact number of (Gaussian, tile) pairs K over all B x V views (the reference's `num_rendered`, summed).
- * Enqueues a counting pass and writes K to *pairs_out (a DEVICE int64). Used by callers that cannot afford the
- * worst-case workspace; they synchronise once, size the workspace from K and then call lgm_render_forward. */
+/* Exact pair counts over all B x V views. Enqueues a counting pass and writes pairs_out (a DEVICE int64[2]):
+ *   [0] pairs actually binned (upstream's 3-sigma tile rect minus tiles where alpha < 1/255 is provable for every
+ *       pixel -- the capacity a packed workspace needs), [1] upstream's num_rendered summed over views.
+ * Used by callers that cannot afford the slot workspace; they synchronise once, size the workspace from [0] and
+ * call lgm_render_forward with that pair_capacity. */
 int lgm_render_count_pairs(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
                            const float *cam_view_proj, float tanfovx, float tanfovy, float scale_modifier,
                            void *workspace, size_t workspace_bytes, long long *pairs_out, void *stream);
 
 /* Forward of all B x V renders (replaces B*V calls of _C.rasterize_gaussians). radii_out [B,V,N] int32 may be
- * NULL. stats_out, if not NULL, is a DEVICE int64[2]: {K = total pairs, overflow flag}. */
+ * NULL. stats_out, if not NULL, is a DEVICE int64[2] with the counts described at lgm_render_count_pairs. */
 int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
                        const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                        float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
@@ -64,6 +67,21 @@ int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussian
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
                         float *d_gaussians, float *d_means2D, void *workspace, size_t workspace_bytes,
                         long long pair_capacity, void *stream);
+
+/* Diagnostics: while device_counters (a DEVICE uint64[8], caller-zeroed) is set, the render kernels add work
+ * counts to it: [0] forward wavefront-entry iterations, [1] accepted (pixel, Gaussian) contributions,
+ * [2] backward wavefront-entry iterations, [3] backward (pixel, Gaussian) gradient contributions,
+ * [4] dense / [5] sparse wavefront reductions, [6] tile-list entries staged by the forward, [7] max forward
+ * iterations of one wavefront; then per tile workgroup (B*V*T of them) 4 s_memrealtime stamps (100 MHz):
+ * [8+4t] fwd start, [8+4t+1] fwd end, [8+4t+2] bwd start (after the early exit test), [8+4t+3] bwd end -- so
+ * the buffer must hold 8 + 4*B*V*tiles entries. NULL disables (default). Process-wide; not for concurrent use. */
+int lgm_render_debug_counters(unsigned long long *device_counters);
+
+/* Option flags (process-wide, default 0). LGM_RENDER_NO_CULL bins upstream's full 3-sigma tile rects instead of
+ * dropping (Gaussian, tile) pairs where alpha < 1/255 is provable for every pixel; outputs are identical either
+ * way (tests/test_render_gpu.py::test_exact_culling_is_output_preserving), only the work differs. */
+#define LGM_RENDER_NO_CULL 1
+int lgm_render_set_flags(int flags);
 
 #ifdef __cplusplus
 }

@@ -11,7 +11,8 @@ import os
 
 import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "liblgm_amd.so")
+LIB_PATH = os.environ.get("LGM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                          "liblgm_amd.so")
 
 _c_int, _c_ll, _c_float, _c_size, _vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 
@@ -29,6 +30,8 @@ SIGNATURES = {
     "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _c_size, _vp]),
     "lgm_attn_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "lgm_render_debug_counters": (_c_int, [_vp]),
+    "lgm_render_set_flags": (_c_int, [_c_int]),
     "lgm_profiler_create": (_vp, []),
     "lgm_profiler_attach": (_c_int, [_vp]),
     "lgm_profiler_summary": (_c_int, [_vp, ctypes.c_char_p, _c_size]),

@@ -8,7 +8,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = ["csrc/common.hip", "csrc/render.hip", "csrc/attention.hip"]
+SOURCES = ["csrc/common.hip", "csrc/render_bin.hip", "csrc/render_raster.hip", "csrc/render_api.hip",
+           "csrc/attention.hip"]
 OUT = os.path.join(HERE, "_lib", "liblgm_amd.so")
 ARCH = os.environ.get("LGM_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -22,27 +23,32 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = sources() + [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
+    deps = sources() + [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))] + \
+        [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str = None, defines=()) -> str:
+    """Compile every source and link the shared library (`out` and `defines` build A/B variants)."""
+    out = out or OUT
+    if out == OUT and not force and not needs_build():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     objs = []
+    tag = "" if out == OUT else "." + os.path.basename(out)
     for src in sources():
-        obj = os.path.join(HERE, "_lib", os.path.basename(src) + ".o")
+        obj = os.path.join(HERE, "_lib", os.path.basename(src) + tag + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-               "-munsafe-fp-atomics", "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+               "-munsafe-fp-atomics", "-fno-slp-vectorize", "-I", os.path.join(ROOT, "include"), "-I",
+               os.path.join(HERE, "csrc"), "-c", src, "-o", obj] + [f"-D{d}" for d in defines]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = OUT + ".tmp"
+    tmp = out + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

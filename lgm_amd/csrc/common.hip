@@ -4,7 +4,9 @@
 #include <stdarg.h>
 #include <string.h>
 
+#include <atomic>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -12,6 +14,7 @@
 
 struct lgm_profiler {
     struct Rec { const char *name; hipEvent_t a, b; };
+    std::mutex mu;
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     size_t used = 0;
@@ -27,7 +30,7 @@ struct lgm_profiler {
 
 namespace lgm {
 static thread_local char g_err[512] = {0};
-static thread_local lgm_profiler *g_prof = nullptr;
+static std::atomic<lgm_profiler *> g_prof{nullptr};  // process-wide: autograd runs backward on its own thread
 static thread_local const char *g_pending = nullptr;
 static thread_local hipEvent_t g_pending_ev = nullptr;
 
@@ -40,17 +43,21 @@ void set_error(const char *fmt, ...) {
 void clear_error() { g_err[0] = 0; }
 
 void prof_begin(const char *name, hipStream_t st) {
-    if (!g_prof) return;
+    lgm_profiler *p = g_prof.load();
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(p->mu);
     g_pending = name;
-    g_pending_ev = g_prof->get();
-    if (g_pending_ev) hipEventRecord(g_pending_ev, st);
+    g_pending_ev = p->get();
+    if (g_pending_ev) (void)hipEventRecord(g_pending_ev, st);
 }
 void prof_end(hipStream_t st) {
-    if (!g_prof || !g_pending_ev) return;
-    hipEvent_t b = g_prof->get();
+    lgm_profiler *p = g_prof.load();
+    if (!p || !g_pending_ev) return;
+    std::lock_guard<std::mutex> lk(p->mu);
+    hipEvent_t b = p->get();
     if (!b) return;
     (void)hipEventRecord(b, st);
-    g_prof->recs.push_back({g_pending, g_pending_ev, b});
+    p->recs.push_back({g_pending, g_pending_ev, b});
     g_pending_ev = nullptr;
 }
 }  // namespace lgm
@@ -61,11 +68,12 @@ int lgm_abi_version(void) { return 1; }
 
 lgm_profiler *lgm_profiler_create(void) { return new lgm_profiler(); }
 int lgm_profiler_attach(lgm_profiler *p) {
-    lgm::g_prof = p;
+    lgm::g_prof.store(p);
     return LGM_OK;
 }
 int lgm_profiler_reset(lgm_profiler *p) {
     if (!p) return LGM_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     p->recs.clear();
     p->used = 0;
     return LGM_OK;
@@ -102,7 +110,7 @@ int lgm_profiler_summary(lgm_profiler *p, char *buf, size_t len) {
 }
 void lgm_profiler_destroy(lgm_profiler *p) {
     if (!p) return;
-    if (lgm::g_prof == p) lgm::g_prof = nullptr;
+    if (lgm::g_prof.load() == p) lgm::g_prof.store(nullptr);
     for (auto e : p->pool) (void)hipEventDestroy(e);
     delete p;
 }

@@ -1,0 +1,293 @@
+// lgm_amd/csrc/render_common.h -- shared constants, workspace layout and device math of the render path.
+//
+// Numerics restate SURVEY.md §2.3 (the upstream algorithm behind core/gs.py:58-85; CPU restatement in
+// oracle/raster_oracle.c): 0.3 dilation, 1.3 tanfov clamp inside J, depth cull 0.2, radius = ceil(3 sqrt(lmax))
+// with max(0.1, mid^2 - det), ndc2Pix in double, integer tile-rect math, alpha cap 0.99 / floor 1/255,
+// transmittance floor 1e-4 tested before accumulation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+#include "lgm_render.h"
+
+namespace lgm {
+
+constexpr int BX = 16, BY = 16, TILE_PIX = BX * BY;  // 256 pixels per tile = 4 wavefronts (8x8 quadrants)
+constexpr int NACC = 10;                             // per-(view, Gaussian) screen-space gradient record
+constexpr int LDS_HIST_MAX = 8192;                   // tiles per view for the LDS-histogram binning path
+constexpr float LOG2E = 1.4426950408889634f;
+
+inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Workspace layout. Pair storage `pairs` holds one u64 key (depth_bits << 32 | gaussian id) per (Gaussian, tile)
+// pair; after sorting, the tile's u32 ids are written in place at the start of its range.
+//   slot mode   (pair_capacity <= 0): tile (bv, t) owns pairs[(bv*T + t) * N, +N): no counting pass, no scan.
+//   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
+struct Layout {
+    size_t gA, gB, gD, rects, tile_count, tile_start, pairs, final_T, n_contrib, accum, misc, total;
+    long long cap;
+    bool slot;
+};
+
+inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capacity) {
+    const size_t BV = (size_t)B * V, T = (size_t)((W + BX - 1) / BX) * ((H + BY - 1) / BY), P = (size_t)H * W;
+    Layout L;
+    L.slot = pair_capacity <= 0;
+    L.cap = L.slot ? (long long)(BV * T * (size_t)N) : pair_capacity;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
+    L.gA = take(BV * N * 16);
+    L.gB = take(BV * N * 16);
+    L.gD = take(BV * N * 4);
+    L.rects = take(BV * N * 8);
+    L.tile_count = take(BV * T * 4);
+    L.tile_start = take((BV * T + 1) * 4);
+    L.pairs = take((size_t)L.cap * 8);
+    L.final_T = take(BV * P * 4);
+    L.n_contrib = take(BV * P * 4);
+    L.accum = take(BV * N * NACC * 4);
+    L.misc = take(64);
+    L.total = o;
+    return L;
+}
+
+struct Dims {
+    int B, V, N, H, W, gx, gy, T, BV;
+    float tanx, tany, fx, fy, mod;
+    unsigned long long *counters;  // optional device u64[8] work counters (see lgm_render_debug_counters), or null
+    int flags;                     // LGM_RENDER_NO_CULL: bin upstream's full 3-sigma rects (no exact culling)
+};
+
+// ------------------------------------------------------------------------------------------------------------
+// Camera helpers: the 4x4 matrices are the row-major torch tensors of core/gs.py:54-55 read column-major.
+__device__ __forceinline__ void xf43(const float *M, float x, float y, float z, float o[3]) {
+    o[0] = M[0] * x + M[4] * y + M[8] * z + M[12];
+    o[1] = M[1] * x + M[5] * y + M[9] * z + M[13];
+    o[2] = M[2] * x + M[6] * y + M[10] * z + M[14];
+}
+__device__ __forceinline__ void xf44(const float *M, float x, float y, float z, float o[4]) {
+    o[0] = M[0] * x + M[4] * y + M[8] * z + M[12];
+    o[1] = M[1] * x + M[5] * y + M[9] * z + M[13];
+    o[2] = M[2] * x + M[6] * y + M[10] * z + M[14];
+    o[3] = M[3] * x + M[7] * y + M[11] * z + M[15];
+}
+
+// glm-convention rotation matrix R[col][row] from the un-normalised quaternion (r,x,y,z) (upstream semantics).
+__device__ __forceinline__ void quat_rot(const float q[4], float R[3][3]) {
+    const float r = q[0], x = q[1], y = q[2], z = q[3];
+    R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - r * z); R[0][2] = 2.f * (x * z + r * y);
+    R[1][0] = 2.f * (x * y + r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - r * x);
+    R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+}
+
+// Sigma = M^T M with M = S*R (glm): Sigma[c][r] = sum_k s_k^2 R[c][k] R[r][k]; stored (00,01,02,11,12,22).
+__device__ __forceinline__ void cov3d(const float s[3], const float R[3][3], float c3[6]) {
+    const float s0 = s[0] * s[0], s1 = s[1] * s[1], s2 = s[2] * s[2];
+#define LGM_SIG(c, r) (s0 * R[c][0] * R[r][0] + s1 * R[c][1] * R[r][1] + s2 * R[c][2] * R[r][2])
+    c3[0] = LGM_SIG(0, 0); c3[1] = LGM_SIG(0, 1); c3[2] = LGM_SIG(0, 2);
+    c3[3] = LGM_SIG(1, 1); c3[4] = LGM_SIG(1, 2); c3[5] = LGM_SIG(2, 2);
+#undef LGM_SIG
+}
+
+// The two non-zero glm columns of T = W*J (with the 1.3 tanfov clamp on t), SURVEY §2.3 row 1.
+struct ProjCtx {
+    float T0[3], T1[3];  // glm T[0][*], T[1][*]
+    float t[3];          // clamped view-space mean
+    float xmul, ymul;    // 0 where the clamp was active (gradient cut, as upstream)
+};
+__device__ __forceinline__ ProjCtx make_proj(const float *Vw, float mx, float my, float mz, float fx, float fy,
+                                             float tanx, float tany) {
+    ProjCtx P;
+    xf43(Vw, mx, my, mz, P.t);
+    const float limx = 1.3f * tanx, limy = 1.3f * tany;
+    const float txtz = P.t[0] / P.t[2], tytz = P.t[1] / P.t[2];
+    P.t[0] = fminf(limx, fmaxf(-limx, txtz)) * P.t[2];
+    P.t[1] = fminf(limy, fmaxf(-limy, tytz)) * P.t[2];
+    P.xmul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+    P.ymul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+    const float tz = P.t[2];
+    const float J00 = fx / tz, J02 = -(fx * P.t[0]) / (tz * tz);
+    const float J11 = fy / tz, J12 = -(fy * P.t[1]) / (tz * tz);
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        P.T0[r] = Vw[4 * r + 0] * J00 + Vw[4 * r + 2] * J02;
+        P.T1[r] = Vw[4 * r + 1] * J11 + Vw[4 * r + 2] * J12;
+    }
+    return P;
+}
+__device__ __forceinline__ void cov2d(const ProjCtx &P, const float c3[6], float &a, float &b, float &c) {
+    const float S[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
+    float s0[3], s1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        s0[k] = S[k][0] * P.T0[0] + S[k][1] * P.T0[1] + S[k][2] * P.T0[2];
+        s1[k] = S[k][0] * P.T1[0] + S[k][1] * P.T1[1] + S[k][2] * P.T1[2];
+    }
+    a = P.T0[0] * s0[0] + P.T0[1] * s0[1] + P.T0[2] * s0[2] + 0.3f;
+    b = P.T1[0] * s0[0] + P.T1[1] * s0[1] + P.T1[2] * s0[2];
+    c = P.T1[0] * s1[0] + P.T1[1] * s1[1] + P.T1[2] * s1[2] + 0.3f;
+}
+
+__device__ __forceinline__ float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+// Can any integer pixel of [rx0, rx1] x [ry0, ry1] reach q = A dx^2 + 2B dx dy + C dy^2 <= tau around (x, y)?
+// Exact minimum of the (convex) quadratic over the rectangle: 0 if the centre is inside, else the minimum over the
+// four edges (1-D minimiser clamped to the edge). Conservative for the integer pixels it contains.
+// invA = 1/A, invC = 1/C (precomputed once per Gaussian).
+__device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float A, float B, float C, float invA,
+                                                  float invC, float tau, float rx0, float rx1, float ry0, float ry1) {
+    if (tau >= 3.0e38f) return true;
+    if (x >= rx0 && x <= rx1 && y >= ry0 && y <= ry1) return true;
+    float best = 3.0e38f;
+    const float ex[2] = {rx0, rx1}, ey[2] = {ry0, ry1};
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const float dx = x - ex[e];
+        const float dy = fminf(fmaxf(-B * dx * invC, y - ry1), y - ry0);
+        best = fminf(best, A * dx * dx + 2.f * B * dx * dy + C * dy * dy);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const float dy = y - ey[e];
+        const float dx = fminf(fmaxf(-B * dy * invA, x - rx1), x - rx0);
+        best = fminf(best, A * dx * dx + 2.f * B * dx * dy + C * dy * dy);
+    }
+    return best <= tau;
+}
+
+struct Geo {
+    float x, y, depth, A, B, C, opacity;  // pixel centre, view depth, conic (A, B, C), opacity
+    float hx, hy;                         // half-extents of the alpha >= 1/255 ellipse's bounding box (pixels)
+    float tau;                            // inflated alpha >= 1/255 threshold on q (3e38: never cull)
+    int x0, y0, x1, y1;                   // reference tile rect (3-sigma)
+    int cx0, cy0, cx1, cy1;               // emitted tile rect: reference rect ∩ tiles the alpha ellipse can reach
+    int radius;
+};
+
+// Per-Gaussian forward preprocess. Returns false if culled (radius 0 upstream).
+//
+// Exact opacity-aware tile culling: upstream keeps every tile of the 3-sigma rect, but a tile in which
+// alpha = min(0.99, o exp(-q/2)) < 1/255 for every pixel is skipped by every pixel (`continue`), changing
+// nothing but the internal contributor counter. alpha >= 1/255 <=> q <= tau = 2 ln(255 o); the ellipse
+// {q <= tau} lies inside |dx| <= sqrt(tau a), |dy| <= sqrt(tau c) (a, c: the dilated 2D covariance), which
+// bounds the candidate tiles; the emitter then keeps a tile only if ellipse_hits_rect() says some pixel of it
+// can reach q <= tau. tau is inflated (below) so fp32 rounding of q can never re-admit a culled pixel.
+__device__ __forceinline__ bool preprocess_one(const float *g, const float *Vw, const float *Pm, const Dims &d,
+                                               Geo &o) {
+    float hom[4], pv[3];
+    xf44(Pm, g[0], g[1], g[2], hom);
+    const float pw = 1.0f / (hom[3] + 0.0000001f);
+    const float ppx = hom[0] * pw, ppy = hom[1] * pw;
+    xf43(Vw, g[0], g[1], g[2], pv);
+    if (pv[2] <= 0.2f) return false;
+    float R[3][3];
+    const float q[4] = {g[7], g[8], g[9], g[10]};
+    quat_rot(q, R);
+    const float s[3] = {d.mod * g[4], d.mod * g[5], d.mod * g[6]};
+    float c3[6];
+    cov3d(s, R, c3);
+    const ProjCtx P = make_proj(Vw, g[0], g[1], g[2], d.fx, d.fy, d.tanx, d.tany);
+    float a, b, c;
+    cov2d(P, c3, a, b, c);
+    const float det = a * c - b * b;
+    if (det == 0.0f) return false;
+    const float det_inv = 1.f / det;
+    const float mid = 0.5f * (a + c);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float rad = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    const float px = ndc2pix(ppx, d.W), py = ndc2pix(ppy, d.H);
+    const int r = (int)rad;
+    const int x0 = min(d.gx, max(0, (int)((px - r) / BX)));
+    const int y0 = min(d.gy, max(0, (int)((py - r) / BY)));
+    const int x1 = min(d.gx, max(0, (int)((px + r + BX - 1) / BX)));
+    const int y1 = min(d.gy, max(0, (int)((py + r + BY - 1) / BY)));
+    if ((x1 - x0) * (y1 - y0) == 0) return false;
+    o.x = px; o.y = py; o.depth = pv[2];
+    o.A = c * det_inv; o.B = -b * det_inv; o.C = a * det_inv;
+    o.opacity = g[3];
+    o.x0 = x0; o.y0 = y0; o.x1 = x1; o.y1 = y1; o.radius = r;
+    // --- exact opacity-aware cull of the emitted rect
+    const float op = g[3];
+    if (d.flags & LGM_RENDER_NO_CULL) {
+        o.hx = o.hy = 3.0e38f;
+        o.tau = 3.0e38f;
+        o.cx0 = x0; o.cx1 = x1; o.cy0 = y0; o.cy1 = y1;
+        return true;
+    }
+    if (!(op * 255.0f > 1.0f)) {  // o <= 1/255: alpha < 1/255 everywhere (and NaN-safe)
+        o.hx = o.hy = -1.f;
+        o.tau = -1.f;
+        o.cx0 = o.cx1 = x0; o.cy0 = o.cy1 = y0;
+        return true;
+    }
+    // fp32 evaluation of q = A dx^2 + 2B dx dy + C dy^2 loses ~eps * kappa relative accuracy on elongated
+    // ellipses; cond = (a + c)^2 / det ~ kappa. Inflate tau by 1e-3 + 2e-5 * cond (>= 80x the rounding bound) and
+    // do not cull ill-conditioned or non-positive-definite ones at all (keep upstream's full rect).
+    const float cond = (a + c) * (a + c) / det;
+    if (!(det > 0.f) || !(cond < 4e4f)) {
+        o.hx = o.hy = 3.0e38f;
+        o.tau = 3.0e38f;
+        o.cx0 = x0; o.cx1 = x1; o.cy0 = y0; o.cy1 = y1;
+        return true;
+    }
+    const float tau = 2.0f * logf(255.0f * op) * (1.001f + 2e-5f * cond) + 1e-3f;
+    o.tau = tau;
+    o.hx = sqrtf(tau * fmaxf(a, 0.f));
+    o.hy = sqrtf(tau * fmaxf(c, 0.f));
+    const float lx = fmaxf(-1.0f, fminf((float)d.gx, (px - o.hx - (BX - 1)) / BX));
+    const float hxt = fmaxf(-1.0f, fminf((float)d.gx, (px + o.hx) / BX));
+    const float ly = fmaxf(-1.0f, fminf((float)d.gy, (py - o.hy - (BY - 1)) / BY));
+    const float hyt = fmaxf(-1.0f, fminf((float)d.gy, (py + o.hy) / BY));
+    o.cx0 = max(x0, (int)ceilf(lx));
+    o.cx1 = min(x1, (int)floorf(hxt) + 1);
+    o.cy0 = max(y0, (int)ceilf(ly));
+    o.cy1 = min(y1, (int)floorf(hyt) + 1);
+    if (o.cx1 < o.cx0) o.cx1 = o.cx0;
+    if (o.cy1 < o.cy0) o.cy1 = o.cy0;
+    return true;
+}
+
+__device__ __forceinline__ void load_gaussian(const float *__restrict__ src, float g[14]) {
+    // rows are 56 B, always 8-B aligned: 7 x dwordx2
+    const float2 *p = reinterpret_cast<const float2 *>(src);
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        const float2 v = p[k];
+        g[2 * k] = v.x;
+        g[2 * k + 1] = v.y;
+    }
+}
+
+// Tile bucket of one (view, tile): base offset into `pairs` and entry count.
+// slot_stride < 0 selects packed mode; slot mode uses stride N (possibly 0: then every bucket is empty).
+__device__ __forceinline__ void tile_range(int tile, long long slot_stride, const int *__restrict__ tile_start,
+                                           const int *__restrict__ tile_count, long long &base, int &n) {
+    if (slot_stride >= 0) {
+        base = (long long)tile * slot_stride;
+        n = tile_count[tile];
+    } else {
+        base = tile_start[tile];
+        n = tile_start[tile + 1] - tile_start[tile];
+    }
+}
+
+// Pixel of thread t inside a 16x16 tile: wavefront w owns the 8x8 quadrant (w & 1, w >> 1).
+__device__ __forceinline__ void tile_pixel(int t, int &lx, int &ly) {
+    const int w = t >> 6, l = t & 63;
+    lx = ((w & 1) << 3) + (l & 7);
+    ly = ((w >> 1) << 3) + (l >> 3);
+}
+
+// ---- host launchers (defined in render_bin.hip / render_raster.hip)
+int launch_binning(const Dims &d, const float *gaussians, const float *cam_view, const float *cam_view_proj,
+                   char *ws, const Layout &L, int *radii_out, long long *stats_out, bool count_only,
+                   hipStream_t st);
+int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, float *image, float *depth,
+                      float *alpha, char *ws, const Layout &L, hipStream_t st);
+int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_view, const float *cam_view_proj,
+                      const float *bg, const float *d_image, const float *d_depth, const float *d_alpha,
+                      float *d_gaussians, float *d_means2D, char *ws, const Layout &L, hipStream_t st);
+
+}  // namespace lgm

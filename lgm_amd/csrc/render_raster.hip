@@ -1,0 +1,587 @@
+// lgm_amd/csrc/render_raster.hip -- per-tile alpha compositing (forward), its reverse-order gradient pass, and
+// the per-Gaussian projection backward.
+//
+// One 256-thread workgroup per 16x16 tile; wavefront w owns the 8x8 quadrant (w & 1, w >> 1). The tile's sorted
+// Gaussians are staged 256 at a time in LDS; the loader thread of each entry also tests the entry's alpha >= 1/255
+// bounding box (render_common.h) against the four quadrants, and every wavefront then compacts the batch to the
+// entries that can touch its quadrant (ballot + popcount prefix), so it only iterates over Gaussians for which
+// some of its pixels pass upstream's `alpha >= 1/255` test. Per-pixel arithmetic, thresholds, the early
+// termination and the reverse recurrences are upstream's; exp uses v_exp_f32 (exp2 with a log2(e) prescale).
+#include "render_common.h"
+
+#ifndef LGM_BWD_BU
+#define LGM_BWD_BU 2  // backward entries evaluated per step (ILP vs registers)
+#endif
+
+namespace lgm {
+namespace {
+
+__device__ __forceinline__ unsigned long long lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
+
+__device__ __forceinline__ int __reduce_add_wave(unsigned v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (unsigned)__shfl_xor((int)v, o, 64);
+    return (int)v;
+}
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+
+// Stage entries [b0, b0 + 256) of the tile's list (fwd: front-to-back; bwd: reversed) and build the per-wave
+// compacted lists. Returns this wave's list length.
+constexpr int SENT = TILE_PIX;  // sentinel slot: opacity 0, never contributes (pads the per-wave lists)
+struct Stage {
+    float4 P[TILE_PIX + 1];  // x, y, A, B
+    float2 Q[TILE_PIX + 1];  // C, opacity
+    float4 R[TILE_PIX + 1];  // r, g, b, depth
+    unsigned id[TILE_PIX];
+    unsigned char mask[TILE_PIX];
+    unsigned short list[4][TILE_PIX + 4];  // per-wave compacted entry indices, padded with SENT to a multiple of 4
+};
+
+__device__ __forceinline__ void stage_entry(Stage &S, int j, bool have, unsigned gid, size_t gbase, int b, int N,
+                                            int tx0, int ty0, const float4 *__restrict__ gA,
+                                            const float4 *__restrict__ gB, const float *__restrict__ gD,
+                                            const float *__restrict__ gauss) {
+    unsigned char mask = 0;
+    if (have) {
+        const float4 a = gA[gbase + gid];
+        const float4 bb = gB[gbase + gid];
+        const float dep = gD[gbase + gid];
+        const float *c = gauss + ((size_t)b * N + gid) * 14 + 11;
+        S.P[j] = make_float4(a.x, a.y, bb.x, bb.y);
+        S.Q[j] = make_float2(bb.z, bb.w);
+        S.R[j] = make_float4(c[0], c[1], c[2], dep);
+        S.id[j] = gid;
+        const float iA = 1.0f / bb.x, iC = 1.0f / bb.z;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float qx = (float)(tx0 + ((q & 1) << 3)), qy = (float)(ty0 + ((q >> 1) << 3));
+            if (ellipse_hits_rect(a.x, a.y, bb.x, bb.y, bb.z, iA, iC, a.z, qx, qx + 7.0f, qy, qy + 7.0f))
+                mask |= (unsigned char)(1u << q);
+        }
+    }
+    S.mask[j] = mask;
+}
+
+__device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin = 0) {
+    int cnt = 0;
+    const unsigned long long lt = lanemask_lt(lane);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int j = c * 64 + lane;
+        const bool bit = ((S.mask[j] >> w) & 1u) && j >= jmin;
+        const unsigned long long bal = __ballot(bit);
+        if (bit) S.list[w][cnt + __popcll(bal & lt)] = (unsigned short)j;
+        cnt += __popcll(bal);
+    }
+    if (lane < 4) S.list[w][cnt + lane] = (unsigned short)SENT;  // pad to the next multiple of 4
+    return cnt;
+}
+
+// Four consecutive list entries as wave-uniform (scalar) indices.
+__device__ __forceinline__ void list4(const Stage &S, int w, int kk, int (&jj)[4]) {
+    const uint2 v = *reinterpret_cast<const uint2 *>(&S.list[w][kk]);
+    const unsigned lo = __builtin_amdgcn_readfirstlane(v.x), hi = __builtin_amdgcn_readfirstlane(v.y);
+    jj[0] = lo & 0xffffu;
+    jj[1] = lo >> 16;
+    jj[2] = hi & 0xffffu;
+    jj[3] = hi >> 16;
+}
+
+__device__ __forceinline__ void init_sentinel(Stage &S) {
+    if (threadIdx.x == 0) {
+        S.P[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
+        S.Q[SENT] = make_float2(0.f, 0.f);
+        S.R[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+// k_render_fwd: grid (B*V*T), block 256.
+__global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_stride, const int *__restrict__ tile_start,
+                                                    const int *__restrict__ tile_count,
+                                                    const unsigned long long *__restrict__ pairs,
+                                                    const float4 *__restrict__ gA, const float4 *__restrict__ gB,
+                                                    const float *__restrict__ gD, const float *__restrict__ gauss,
+                                                    const float *__restrict__ bg, float *__restrict__ out_img,
+                                                    float *__restrict__ out_depth, float *__restrict__ out_alpha,
+                                                    float *__restrict__ final_T, int *__restrict__ n_contrib) {
+    __shared__ Stage S;
+    const int tile = blockIdx.x;
+    const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
+    const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    int lx, ly;
+    tile_pixel(tid, lx, ly);
+    const int px = tx0 + lx, py = ty0 + ly;
+    const bool inside = px < d.W && py < d.H;
+    const float pfx = (float)px, pfy = (float)py;
+    long long base;
+    int n;
+    tile_range(tile, slot_stride, tile_start, tile_count, base, n);
+    const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base);
+    const size_t gbase = (size_t)bv * d.N;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    init_sentinel(S);
+    bool done = !inside;
+    float Tr = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
+    int last = 0;
+    constexpr int FU = 4;
+    unsigned c_iter = 0, c_acc = 0, c_list = 0;  // diagnostic work counters (Dims::counters)
+    for (int b0 = 0; b0 < n; b0 += TILE_PIX) {
+        if (__syncthreads_count(done) == TILE_PIX) break;
+        c_list += min(TILE_PIX, n - b0);
+        const int k = b0 + tid;
+        stage_entry(S, tid, k < n, k < n ? ids[k] : 0u, gbase, b, d.N, tx0, ty0, gA, gB, gD, gauss);
+        __syncthreads();
+        const int cnt = compact_wave(S, w, lane);
+        // FU = 4 entries per step: their alphas are independent of the running transmittance, so they are evaluated
+        // together (ILP, branch-free: list padded with the opacity-0 sentinel); only the short T / colour update
+        // chain stays serial, in list order, as upstream.
+        for (int kk = 0; kk < cnt; kk += FU) {
+            if (__ballot(!done) == 0ull) break;
+            c_iter += min(FU, cnt - kk);
+            int jj[FU];
+            list4(S, w, kk, jj);
+            float al[FU];
+            float4 cc[FU];
+#pragma unroll
+            for (int u = 0; u < FU; u++) {
+                const float4 P = S.P[jj[u]];
+                const float2 Q = S.Q[jj[u]];
+                cc[u] = S.R[jj[u]];
+                const float dx = P.x - pfx, dy = P.y - pfy;
+                const float power = -0.5f * (P.z * dx * dx + Q.x * dy * dy) - P.w * dx * dy;
+                const float alpha = fminf(0.99f, Q.y * __builtin_amdgcn_exp2f(power * LOG2E));
+                al[u] = (power > 0.0f || alpha < 1.0f / 255.0f) ? 0.f : alpha;  // 0 == skipped
+            }
+#pragma unroll
+            for (int u = 0; u < FU; u++) {
+                if (done || al[u] == 0.f) continue;
+                const float alpha = al[u];
+                const float test_T = Tr * (1 - alpha);
+                if (test_T < 0.0001f) {
+                    done = true;
+                    continue;
+                }
+                C0 += cc[u].x * alpha * Tr;
+                C1 += cc[u].y * alpha * Tr;
+                C2 += cc[u].z * alpha * Tr;
+                D += cc[u].w * alpha * Tr;
+                Tr = test_T;
+                last = b0 + jj[u] + 1;
+                c_acc++;
+            }
+        }
+    }
+    if (d.counters) {
+        c_acc = (unsigned)__reduce_add_wave(c_acc);
+        if (lane == 0) {
+            atomicAdd(&d.counters[0], (unsigned long long)c_iter);
+            atomicAdd(&d.counters[1], (unsigned long long)c_acc);
+            if (w == 0) atomicAdd(&d.counters[6], (unsigned long long)c_list);
+            atomicMax(&d.counters[7], (unsigned long long)c_iter);
+        }
+        if (tid == 0) {  // per-workgroup timeline (100 MHz s_memrealtime ticks): [8 + 4*tile] start, +1 end
+            d.counters[8 + 4 * (size_t)tile] = t_start;
+            d.counters[8 + 4 * (size_t)tile + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    if (inside) {
+        const size_t P = (size_t)d.H * d.W;
+        const size_t pid = (size_t)d.W * py + px;
+        final_T[bv * P + pid] = Tr;
+        n_contrib[bv * P + pid] = last;
+        float *img = out_img + (size_t)bv * 3 * P;
+        img[pid] = C0 + Tr * bg[0];
+        img[P + pid] = C1 + Tr * bg[1];
+        img[2 * P + pid] = C2 + Tr * bg[2];
+        out_depth[bv * P + pid] = D;
+        out_alpha[bv * P + pid] = 1 - Tr;
+    }
+}
+
+// Sum over each 16-lane DPP row (quad_perm, row_half_mirror, row_mirror): every lane ends with its row's sum.
+#define LGM_DPP_ADD(v, ctrl)                                                                                   \
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), ctrl, 0xf, 0xf, false))
+__device__ __forceinline__ float row_sum16(float v) {
+    LGM_DPP_ADD(v, 0xB1);   // quad_perm [1,0,3,2]
+    LGM_DPP_ADD(v, 0x4E);   // quad_perm [2,3,0,1]
+    LGM_DPP_ADD(v, 0x141);  // row_half_mirror
+    LGM_DPP_ADD(v, 0x140);  // row_mirror
+    return v;
+}
+
+// k_render_bwd: grid (B*V*T), block 256. DEPTH: an upstream depth gradient is present (LGM passes none).
+template <bool DEPTH>
+__global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_stride, const int *__restrict__ tile_start,
+                                                    const int *__restrict__ tile_count,
+                                                    const unsigned long long *__restrict__ pairs,
+                                                    const float4 *__restrict__ gA, const float4 *__restrict__ gB,
+                                                    const float *__restrict__ gD, const float *__restrict__ gauss,
+                                                    const float *__restrict__ bg, const float *__restrict__ final_T,
+                                                    const int *__restrict__ n_contrib,
+                                                    const float *__restrict__ d_img,
+                                                    const float *__restrict__ d_depth,
+                                                    const float *__restrict__ d_alpha, float *__restrict__ accum) {
+    constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
+    constexpr int LS = TILE_PIX + 1;             // padded LDS row stride (no bank conflicts)
+    __shared__ Stage S;
+    __shared__ float sAcc[LS * NACC];
+    __shared__ int sMaxLast;
+    const int tile = blockIdx.x;
+    const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
+    const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    int lx, ly;
+    tile_pixel(tid, lx, ly);
+    const int px = tx0 + lx, py = ty0 + ly;
+    const bool inside = px < d.W && py < d.H;
+    const float pfx = (float)px, pfy = (float)py;
+    long long base;
+    int n;
+    tile_range(tile, slot_stride, tile_start, tile_count, base, n);
+    const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base);
+    const size_t P = (size_t)d.H * d.W;
+    const size_t pid = inside ? (size_t)d.W * py + px : 0;
+    const float T_final = inside ? final_T[bv * P + pid] : 0.f;
+    const int last = inside ? n_contrib[bv * P + pid] : 0;
+    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, dpd = 0.f, dpa = 0.f;
+    if (inside) {
+        const float *di = d_img + (size_t)bv * 3 * P;
+        dp0 = di[pid];
+        dp1 = di[P + pid];
+        dp2 = di[2 * P + pid];
+        if (DEPTH) dpd = d_depth[bv * P + pid];
+        if (d_alpha) dpa = d_alpha[bv * P + pid];
+    }
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    init_sentinel(S);
+    if (tid == 0) sMaxLast = 0;
+    __syncthreads();
+    const int wlast = wave_max_i32(last);  // entries at positions >= wlast touch no pixel of this wave
+    if (lane == 0 && wlast > 0) atomicMax(&sMaxLast, wlast);
+    __syncthreads();
+    const int nlist = min(n, sMaxLast);  // entries behind every pixel's last contributor are never visited
+    if (nlist == 0) return;
+    const float bg_dot = bg[0] * dp0 + bg[1] * dp1 + bg[2] * dp2;
+    const float ddelx_dx = 0.5f * d.W, ddely_dy = 0.5f * d.H;
+    float Tr = T_final;
+    float acc_r0 = 0, acc_r1 = 0, acc_r2 = 0, acc_d = 0, acc_a = 0;
+    float last_alpha = 0, lc0 = 0, lc1 = 0, lc2 = 0, last_depth = 0;
+    const size_t gbase = (size_t)bv * d.N;
+    const int ql = lane & 15;
+    constexpr int BU = LGM_BWD_BU;
+    unsigned c_iter = 0, c_valid = 0, c_dense = 0, c_sparse = 0;
+
+    for (int b0 = 0; b0 < nlist; b0 += TILE_PIX) {
+        __syncthreads();
+        const int k = b0 + tid;  // counted from the back
+        stage_entry(S, tid, k < nlist, k < nlist ? ids[nlist - 1 - k] : 0u, gbase, b, d.N, tx0, ty0, gA, gB, gD,
+                    gauss);
+#pragma unroll
+        for (int q = 0; q < NV; q++) sAcc[q * LS + tid] = 0.f;
+        __syncthreads();
+        // position nlist - 1 - (b0 + j) < wlast  <=>  j >= nlist - wlast - b0
+        const int cnt = compact_wave(S, w, lane, nlist - wlast - b0);
+        c_iter += cnt;
+        // BU entries per step: G, alpha and the G-derivatives are independent of the per-pixel recurrences, so
+        // they are evaluated together (ILP); the T / suffix-accumulator recurrences stay serial in list order.
+        for (int kk = 0; kk < cnt; kk += BU) {
+            int jj4[4];
+            list4(S, w, kk & ~3, jj4);
+            int jj[BU];
+#pragma unroll
+            for (int u = 0; u < BU; u++) jj[u] = jj4[(kk & 3) + u];
+            float al[BU], Gv[BU], ex[BU], ey[BU], inv[BU];
+            float4 cc[BU];
+            float v[BU][NACC];
+#pragma unroll
+            for (int u = 0; u < BU; u++) {
+                al[u] = 0.f;
+#pragma unroll
+                for (int q = 0; q < NACC; q++) v[u][q] = 0.f;
+                const int pos = nlist - 1 - (b0 + jj[u]);  // 0-based position in the tile list
+                const float4 Pj = S.P[jj[u]];
+                const float2 Q = S.Q[jj[u]];
+                cc[u] = S.R[jj[u]];
+                const float dx = Pj.x - pfx, dy = Pj.y - pfy;
+                const float power = -0.5f * (Pj.z * dx * dx + Q.x * dy * dy) - Pj.w * dx * dy;
+                const float G = __builtin_amdgcn_exp2f(power * LOG2E);
+                const float alpha = fminf(0.99f, Q.y * G);
+                const bool ok = pos < last && power <= 0.0f && alpha >= 1.0f / 255.0f;
+                al[u] = ok ? alpha : 0.f;
+                Gv[u] = Q.y;  // opacity: dL/dG = opacity * dL/dopa
+                const float gdx = G * dx, gdy = G * dy;
+                // dG/d(mean2D) in pixels, and the conic partials share these
+                ex[u] = -gdx * Pj.z - gdy * Pj.w;
+                ey[u] = -gdy * Q.x - gdx * Pj.w;
+                v[u][2] = -0.5f * gdx * dx;  // scaled by dL/dG below
+                v[u][3] = -0.5f * gdx * dy;
+                v[u][4] = -0.5f * gdy * dy;
+                v[u][5] = G;  // scaled by dL/dopa below
+                // 1 / (1 - alpha): v_rcp_f32 + one Newton step (~0.5 ulp, like the IEEE division upstream uses)
+                const float om = 1.f - alpha;
+                float r = __builtin_amdgcn_rcpf(om);
+                inv[u] = fmaf(fmaf(-om, r, 1.0f), r, r);
+            }
+#pragma unroll
+            for (int u = 0; u < BU; u++) {
+                if (al[u] == 0.f) {
+#pragma unroll
+                    for (int q = 0; q < NACC; q++) v[u][q] = 0.f;
+                    continue;
+                }
+                const float alpha = al[u];
+                const float4 c = cc[u];
+                Tr = Tr * inv[u];
+                const float dchannel_dcolor = alpha * Tr;
+                float dL_dopa = 0.f;
+                acc_r0 = last_alpha * lc0 + (1.f - last_alpha) * acc_r0;
+                lc0 = c.x;
+                dL_dopa += (c.x - acc_r0) * dp0;
+                acc_r1 = last_alpha * lc1 + (1.f - last_alpha) * acc_r1;
+                lc1 = c.y;
+                dL_dopa += (c.y - acc_r1) * dp1;
+                acc_r2 = last_alpha * lc2 + (1.f - last_alpha) * acc_r2;
+                lc2 = c.z;
+                dL_dopa += (c.z - acc_r2) * dp2;
+                v[u][6] = dchannel_dcolor * dp0;
+                v[u][7] = dchannel_dcolor * dp1;
+                v[u][8] = dchannel_dcolor * dp2;
+                if (DEPTH) {
+                    acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
+                    last_depth = c.w;
+                    dL_dopa += (c.w - acc_d) * dpd;
+                    v[u][9] = dchannel_dcolor * dpd;
+                }
+                acc_a = last_alpha + (1.f - last_alpha) * acc_a;
+                dL_dopa += (1 - acc_a) * dpa;
+                dL_dopa *= Tr;
+                last_alpha = alpha;
+                dL_dopa += (-T_final * inv[u]) * bg_dot;
+                const float dL_dG = Gv[u] * dL_dopa;
+                v[u][0] = dL_dG * ex[u] * ddelx_dx;
+                v[u][1] = dL_dG * ey[u] * ddely_dy;
+                v[u][2] *= dL_dG;
+                v[u][3] *= dL_dG;
+                v[u][4] *= dL_dG;
+                v[u][5] *= dL_dopa;
+            }
+#pragma unroll
+            for (int u = 0; u < BU; u++) {
+                const bool valid = al[u] != 0.f;
+                const unsigned long long bal = __ballot(valid);  // wave-uniform
+                if (bal == 0ull) continue;
+                c_valid += __popcll(bal);
+                const int j = jj[u];
+                if (__popcll(bal) <= 4) {  // sparse: the few active lanes add directly
+                    c_sparse++;
+                    if (valid) {
+#pragma unroll
+                        for (int q = 0; q < NV; q++) atomicAdd(&sAcc[q * LS + j], v[u][q]);
+                    }
+                } else {  // dense: 16-lane DPP row sums, then lane (row, q) adds value q: one ds_add per entry
+                    c_dense++;
+                    float mine = 0.f;
+#pragma unroll
+                    for (int q = 0; q < NV; q++) {
+                        const float rr = row_sum16(v[u][q]);
+                        mine = (ql == q) ? rr : mine;
+                    }
+                    if (ql < NV) atomicAdd(&sAcc[ql * LS + j], mine);
+                }
+            }
+        }
+        __syncthreads();
+        // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
+        // gradient records instead of 64 scattered rows
+#pragma unroll
+        for (int it = 0; it < NACC; it++) {
+            const int f = it * TILE_PIX + tid;
+            const int j = f / NACC, q = f - j * NACC;
+            if (q < NV && b0 + j < nlist) {
+                const float a = sAcc[q * LS + j];
+                if (a != 0.f) atomicAdd(accum + (gbase + S.id[j]) * NACC + q, a);
+            }
+        }
+    }
+    if (d.counters && tid == 0) {
+        d.counters[8 + 4 * (size_t)tile + 2] = t_start;
+        d.counters[8 + 4 * (size_t)tile + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (d.counters && lane == 0) {
+        atomicAdd(&d.counters[2], (unsigned long long)c_iter);
+        atomicAdd(&d.counters[3], (unsigned long long)c_valid);
+        atomicAdd(&d.counters[4], (unsigned long long)c_dense);
+        atomicAdd(&d.counters[5], (unsigned long long)c_sparse);
+    }
+}
+
+// k_preproc_bwd: grid (ceil(N/256), B), block 256. Sums over the scene's views in order (deterministic).
+__global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__restrict__ gauss,
+                                                     const float *__restrict__ views,
+                                                     const float *__restrict__ projs, const uint2 *__restrict__ rects,
+                                                     const float *__restrict__ accum, float *__restrict__ d_gauss,
+                                                     float *__restrict__ d_means2D) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (i >= d.N) return;
+    const float fx = d.fx, fy = d.fy, mod = d.mod;
+    float g[14];
+    load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
+    float R[3][3];
+    const float q4[4] = {g[7], g[8], g[9], g[10]};
+    quat_rot(q4, R);
+    const float s[3] = {mod * g[4], mod * g[5], mod * g[6]};
+    float c3[6];
+    cov3d(s, R, c3);
+    const float Sg[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
+    float dmean[3] = {0, 0, 0}, dcov[6] = {0, 0, 0, 0, 0, 0}, dop = 0, dcol[3] = {0, 0, 0};
+    for (int v = 0; v < d.V; v++) {
+        const int bv = b * d.V + v;
+        const size_t k = (size_t)bv * d.N + i;
+        const uint2 r = rects[k];
+        const bool vis = (r.x & 0xffff) != (r.y & 0xffff);
+        if (!vis) {
+            if (d_means2D) { d_means2D[2 * k] = 0.f; d_means2D[2 * k + 1] = 0.f; }
+            continue;
+        }
+        const float *acc = accum + k * NACC;
+        const float dm2x = acc[0], dm2y = acc[1];
+        const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
+        dop += acc[5];
+        dcol[0] += acc[6]; dcol[1] += acc[7]; dcol[2] += acc[8];
+        const float ddep = acc[9];
+        if (d_means2D) { d_means2D[2 * k] = dm2x; d_means2D[2 * k + 1] = dm2y; }
+        const float *Vw = views + 16 * bv;
+        const float *Pm = projs + 16 * bv;
+        // ---- cov2D backward
+        const ProjCtx Pc = make_proj(Vw, g[0], g[1], g[2], fx, fy, d.tanx, d.tany);
+        float a, bb, c;
+        cov2d(Pc, c3, a, bb, c);
+        const float denom = a * c - bb * bb;
+        float dL_da = 0, dL_db = 0, dL_dc = 0;
+        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+        if (denom2inv != 0) {
+            dL_da = denom2inv * (-c * c * dcx + 2 * bb * c * dcy + (denom - a * c) * dcz);
+            dL_dc = denom2inv * (-a * a * dcz + 2 * a * bb * dcy + (denom - a * c) * dcx);
+            dL_db = denom2inv * 2 * (bb * c * dcx - (denom + 2 * bb * bb) * dcy + a * bb * dcz);
+            const float *t0 = Pc.T0, *t1 = Pc.T1;
+            dcov[0] += (t0[0] * t0[0] * dL_da + t0[0] * t1[0] * dL_db + t1[0] * t1[0] * dL_dc);
+            dcov[3] += (t0[1] * t0[1] * dL_da + t0[1] * t1[1] * dL_db + t1[1] * t1[1] * dL_dc);
+            dcov[5] += (t0[2] * t0[2] * dL_da + t0[2] * t1[2] * dL_db + t1[2] * t1[2] * dL_dc);
+            dcov[1] += 2 * t0[0] * t0[1] * dL_da + (t0[0] * t1[1] + t0[1] * t1[0]) * dL_db + 2 * t1[0] * t1[1] * dL_dc;
+            dcov[2] += 2 * t0[0] * t0[2] * dL_da + (t0[0] * t1[2] + t0[2] * t1[0]) * dL_db + 2 * t1[0] * t1[2] * dL_dc;
+            dcov[4] += 2 * t0[2] * t0[1] * dL_da + (t0[1] * t1[2] + t0[2] * t1[1]) * dL_db + 2 * t1[1] * t1[2] * dL_dc;
+        }
+        float dT0[3], dT1[3];
+#pragma unroll
+        for (int kk = 0; kk < 3; kk++) {
+            const float s0 = Pc.T0[0] * Sg[kk][0] + Pc.T0[1] * Sg[kk][1] + Pc.T0[2] * Sg[kk][2];
+            const float s1 = Pc.T1[0] * Sg[kk][0] + Pc.T1[1] * Sg[kk][1] + Pc.T1[2] * Sg[kk][2];
+            dT0[kk] = 2 * s0 * dL_da + s1 * dL_db;
+            dT1[kk] = 2 * s1 * dL_dc + s0 * dL_db;
+        }
+        const float dJ00 = Vw[0] * dT0[0] + Vw[4] * dT0[1] + Vw[8] * dT0[2];
+        const float dJ02 = Vw[2] * dT0[0] + Vw[6] * dT0[1] + Vw[10] * dT0[2];
+        const float dJ11 = Vw[1] * dT1[0] + Vw[5] * dT1[1] + Vw[9] * dT1[2];
+        const float dJ12 = Vw[2] * dT1[0] + Vw[6] * dT1[1] + Vw[10] * dT1[2];
+        const float tz = 1.f / Pc.t[2], tz2 = tz * tz, tz3 = tz2 * tz;
+        const float dtx = Pc.xmul * -fx * tz2 * dJ02;
+        const float dty = Pc.ymul * -fy * tz2 * dJ12;
+        const float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * Pc.t[0]) * tz3 * dJ02 +
+                          (2 * fy * Pc.t[1]) * tz3 * dJ12;
+        dmean[0] += Vw[0] * dtx + Vw[1] * dty + Vw[2] * dtz;
+        dmean[1] += Vw[4] * dtx + Vw[5] * dty + Vw[6] * dtz;
+        dmean[2] += Vw[8] * dtx + Vw[9] * dty + Vw[10] * dtz;
+        // ---- perspective-divide backward
+        float hom[4];
+        xf44(Pm, g[0], g[1], g[2], hom);
+        const float m_w = 1.0f / (hom[3] + 0.0000001f);
+        const float mul1 = hom[0] * m_w * m_w;
+        const float mul2 = hom[1] * m_w * m_w;
+        dmean[0] += (Pm[0] * m_w - Pm[3] * mul1) * dm2x + (Pm[1] * m_w - Pm[3] * mul2) * dm2y;
+        dmean[1] += (Pm[4] * m_w - Pm[7] * mul1) * dm2x + (Pm[5] * m_w - Pm[7] * mul2) * dm2y;
+        dmean[2] += (Pm[8] * m_w - Pm[11] * mul1) * dm2x + (Pm[9] * m_w - Pm[11] * mul2) * dm2y;
+        // ---- depth backward (exact row 2 of the view matrix)
+        dmean[0] += Vw[2] * ddep;
+        dmean[1] += Vw[6] * ddep;
+        dmean[2] += Vw[10] * ddep;
+    }
+    // ---- cov3D backward, once on the view-summed dL/dcov3D (linear, so equal to the per-view sum)
+    const float dS[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
+                            {0.5f * dcov[1], dcov[3], 0.5f * dcov[4]},
+                            {0.5f * dcov[2], 0.5f * dcov[4], dcov[5]}};
+    float dM[3][3];  // dM[c][r] = 2 s_r sum_k R[k][r] dS[c][k]   (glm M = S*R, M[k][r] = s_r R[k][r])
+#pragma unroll
+    for (int cc = 0; cc < 3; cc++)
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++)
+            dM[cc][rr] = 2.0f * s[rr] * (R[0][rr] * dS[cc][0] + R[1][rr] * dS[cc][1] + R[2][rr] * dS[cc][2]);
+    float dscale[3], dd[3][3];
+#pragma unroll
+    for (int ii = 0; ii < 3; ii++) {
+        dscale[ii] = (R[0][ii] * dM[0][ii] + R[1][ii] * dM[1][ii] + R[2][ii] * dM[2][ii]) * mod;
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++) dd[ii][rr] = dM[rr][ii] * s[ii];  // dL_dMt[ii][rr] * s_ii
+    }
+    const float r_ = g[7], x = g[8], y = g[9], z = g[10];
+    float dq[4];
+    dq[0] = 2 * z * (dd[0][1] - dd[1][0]) + 2 * y * (dd[2][0] - dd[0][2]) + 2 * x * (dd[1][2] - dd[2][1]);
+    dq[1] = 2 * y * (dd[1][0] + dd[0][1]) + 2 * z * (dd[2][0] + dd[0][2]) + 2 * r_ * (dd[1][2] - dd[2][1]) -
+            4 * x * (dd[2][2] + dd[1][1]);
+    dq[2] = 2 * x * (dd[1][0] + dd[0][1]) + 2 * r_ * (dd[2][0] - dd[0][2]) + 2 * z * (dd[1][2] + dd[2][1]) -
+            4 * y * (dd[2][2] + dd[0][0]);
+    dq[3] = 2 * r_ * (dd[0][1] - dd[1][0]) + 2 * x * (dd[2][0] + dd[0][2]) + 2 * y * (dd[1][2] + dd[2][1]) -
+            4 * z * (dd[1][1] + dd[0][0]);
+    float *o = d_gauss + ((size_t)b * d.N + i) * 14;
+    const float out[14] = {dmean[0], dmean[1], dmean[2], dop, dscale[0], dscale[1], dscale[2],
+                           dq[0], dq[1], dq[2], dq[3], dcol[0], dcol[1], dcol[2]};
+    float2 *o2 = reinterpret_cast<float2 *>(o);
+#pragma unroll
+    for (int kk = 0; kk < 7; kk++) o2[kk] = make_float2(out[2 * kk], out[2 * kk + 1]);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------------------
+int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, float *image, float *depth,
+                      float *alpha, char *ws, const Layout &L, hipStream_t st) {
+    LGM_LAUNCH("k_render_fwd", st, (k_render_fwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
+                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.tile_start),
+                                       (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
+                                       (const float4 *)(ws + L.gA), (const float4 *)(ws + L.gB),
+                                       (const float *)(ws + L.gD), gaussians, bg, image, depth, alpha,
+                                       (float *)(ws + L.final_T), (int *)(ws + L.n_contrib))));
+    return LGM_OK;
+}
+
+int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_view, const float *cam_view_proj,
+                      const float *bg, const float *d_image, const float *d_depth, const float *d_alpha,
+                      float *d_gaussians, float *d_means2D, char *ws, const Layout &L, hipStream_t st) {
+    if (hipMemsetAsync(ws + L.accum, 0, (size_t)d.BV * d.N * NACC * 4, st) != hipSuccess) {
+        set_error("hipMemsetAsync failed");
+        return LGM_E_HIP;
+    }
+    auto bwd = d_depth ? k_render_bwd<true> : k_render_bwd<false>;
+    LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
+                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.tile_start),
+                                       (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
+                                       (const float4 *)(ws + L.gA), (const float4 *)(ws + L.gB),
+                                       (const float *)(ws + L.gD), gaussians, bg, (const float *)(ws + L.final_T),
+                                       (const int *)(ws + L.n_contrib), d_image, d_depth, d_alpha,
+                                       (float *)(ws + L.accum))));
+    dim3 grid((d.N + 255) / 256, d.B);
+    LGM_LAUNCH("k_preproc_bwd", st, (k_preproc_bwd<<<grid, 256, 0, st>>>(d, gaussians, cam_view, cam_view_proj,
+                                                                        (const uint2 *)(ws + L.rects),
+                                                                        (const float *)(ws + L.accum), d_gaussians,
+                                                                        d_means2D)));
+    return LGM_OK;
+}
+
+}  // namespace lgm

@@ -47,7 +47,7 @@ class _RasterizeBatched(torch.autograd.Function):
                                                    _native.ptr(cam_view_proj), tanx, tany, scale_modifier,
                                                    _native.ptr(ws), small, _native.ptr(k), stream),
                           "lgm_render_count_pairs")
-            cap = max(int(k[0].item()), 1)
+            cap = max(int(k[0].item()), 1)  # pairs actually binned
             ws_bytes = L.lgm_render_workspace_size(B, V, N, H, W, cap)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         image = torch.empty(B, V, 3, H, W, dtype=torch.float32, device=dev)
@@ -58,6 +58,7 @@ class _RasterizeBatched(torch.autograd.Function):
                                            _native.ptr(image), _native.ptr(depth), _native.ptr(alpha), None,
                                            _native.ptr(ws), ws_bytes, cap, None, stream), "lgm_render_forward")
         ctx.save_for_backward(g, cam_view, cam_view_proj, bg)
+        ctx.set_materialize_grads(False)  # unused outputs (LGM never uses depth) arrive as None, not zeros
         ctx.ws, ctx.ws_bytes, ctx.cap = ws, ws_bytes, cap
         ctx.params = (tanx, tany, scale_modifier, H, W)
         return image, depth, alpha
@@ -100,9 +101,9 @@ def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, sc
                                    int(H), int(W))
 
 
-def count_pairs(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scale_modifier=1.0) -> int:
-    """Exact total (Gaussian, tile) pair count K over all B x V views -- the reference's `num_rendered` summed
-    over views (one host sync). Used for byte accounting in bench.py."""
+def count_pairs(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scale_modifier=1.0):
+    """(binned, reference) (Gaussian, tile) pair counts over all B x V views (one host sync): `binned` after the
+    exact opacity-aware tile culling, `reference` = upstream's num_rendered summed over views (SURVEY §8(d)'s K)."""
     L = _native.lib()
     g = gaussians.float().contiguous()
     B, N, V = g.shape[0], g.shape[1], cam_view.shape[1]
@@ -115,7 +116,8 @@ def count_pairs(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scal
     _native.check(L.lgm_render_count_pairs(B, V, N, H, W, _native.ptr(g), _native.ptr(cv), _native.ptr(cvp),
                                            float(tanfovx), float(tanfovy), float(scale_modifier), _native.ptr(ws),
                                            small, _native.ptr(k), _native.stream_of(dev)), "lgm_render_count_pairs")
-    return int(k[0].item())
+    kk = k.tolist()
+    return int(kk[0]), int(kk[1])
 
 
 class GaussianRenderer:

@@ -15,7 +15,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liblgm_oracle.so")
-_lib = None
+_LIB64_PATH = os.path.join(_HERE, "_build", "liblgm_oracle_f64.so")
+_libs = {}
 
 
 def build() -> str:
@@ -23,33 +24,34 @@ def build() -> str:
     return _LIB_PATH
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+def lib(f64: bool = False):
+    if f64 not in _libs:
+        path = _LIB64_PATH if f64 else _LIB_PATH
+        if not os.path.exists(path):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
-        f32p = ctypes.POINTER(ctypes.c_float)
+        L = ctypes.CDLL(path)
+        f32p = ctypes.POINTER(ctypes.c_double if f64 else ctypes.c_float)
+        rp = ctypes.c_double if f64 else ctypes.c_float
         i32p = ctypes.POINTER(ctypes.c_int)
         i64p = ctypes.POINTER(ctypes.c_longlong)
         L.lgm_oracle_render_batch.restype = ctypes.c_int
         L.lgm_oracle_render_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p, f32p, f32p,
-                                              ctypes.c_float, ctypes.c_float, ctypes.c_float, f32p, ctypes.c_int,
+                                              rp, rp, rp, f32p, ctypes.c_int,
                                               ctypes.c_int, f32p, f32p, f32p, i64p, f32p, f32p, f32p, f32p,
                                               ctypes.c_int]
         L.lgm_oracle_render_view.restype = ctypes.c_int
-        L.lgm_oracle_render_view.argtypes = [ctypes.c_int, f32p, f32p, f32p, ctypes.c_float, ctypes.c_float,
-                                             ctypes.c_float, f32p, ctypes.c_int, ctypes.c_int, f32p, f32p, f32p,
+        L.lgm_oracle_render_view.argtypes = [ctypes.c_int, f32p, f32p, f32p, rp, rp,
+                                             rp, f32p, ctypes.c_int, ctypes.c_int, f32p, f32p, f32p,
                                              i32p, i64p, f32p, f32p, f32p, f32p, f32p]
         L.lgm_oracle_preprocess_view.restype = ctypes.c_longlong
-        L.lgm_oracle_preprocess_view.argtypes = [ctypes.c_int, f32p, f32p, f32p, ctypes.c_float, ctypes.c_float,
-                                                 ctypes.c_float, ctypes.c_int, ctypes.c_int, i32p, f32p, f32p,
+        L.lgm_oracle_preprocess_view.argtypes = [ctypes.c_int, f32p, f32p, f32p, rp, rp,
+                                                 rp, ctypes.c_int, ctypes.c_int, i32p, f32p, f32p,
                                                  f32p, i32p]
         L.lgm_oracle_tile_lists.restype = ctypes.c_longlong
-        L.lgm_oracle_tile_lists.argtypes = [ctypes.c_int, f32p, f32p, f32p, ctypes.c_float, ctypes.c_float,
-                                            ctypes.c_float, ctypes.c_int, ctypes.c_int, i32p, i32p, ctypes.c_longlong]
-        _lib = L
-    return _lib
+        L.lgm_oracle_tile_lists.argtypes = [ctypes.c_int, f32p, f32p, f32p, rp, rp,
+                                            rp, ctypes.c_int, ctypes.c_int, i32p, i32p, ctypes.c_longlong]
+        _libs[f64] = L
+    return _libs[f64]
 
 
 def _f(a):
@@ -61,35 +63,37 @@ def _c(a, dtype=np.float32):
 
 
 def render(gaussians, cam_view, cam_view_proj, tanfov: float, H: int, W: int, bg, scale_modifier: float = 1.0,
-           d_image=None, d_depth=None, d_alpha=None, nthreads: int = 0):
+           d_image=None, d_depth=None, d_alpha=None, nthreads: int = 0, f64: bool = False):
     """Forward (+ optional backward) of B x V renders.
 
     gaussians [B,N,14]; cam_view/cam_view_proj [B,V,4,4] (row-major torch layout, as core/gs.py passes them);
     bg [3]. Returns dict with image [B,V,3,H,W] (unclamped), depth/alpha [B,V,1,H,W], K (total pairs),
     evals (pixel-Gaussian evaluations) and, if d_image is given, d_gaussians [B,N,14].
     """
-    g = _c(gaussians)
+    dt = np.float64 if f64 else np.float32
+    g = _c(gaussians, dt)
     B, N = g.shape[0], g.shape[1]
-    views = _c(cam_view).reshape(B, -1, 16)
+    views = _c(cam_view, dt).reshape(B, -1, 16)
     V = views.shape[1]
-    projs = _c(cam_view_proj).reshape(B, V, 16)
-    bgv = _c(bg).reshape(3)
-    color = np.zeros((B, V, 3, H, W), np.float32)
-    depth = np.zeros((B, V, 1, H, W), np.float32)
-    alpha = np.zeros((B, V, 1, H, W), np.float32)
+    projs = _c(cam_view_proj, dt).reshape(B, V, 16)
+    bgv = _c(bg, dt).reshape(3)
+    color = np.zeros((B, V, 3, H, W), dt)
+    depth = np.zeros((B, V, 1, H, W), dt)
+    alpha = np.zeros((B, V, 1, H, W), dt)
     stats = np.zeros(2, np.int64)
     dg = None
     if d_image is not None:
-        d_image = _c(d_image).reshape(B, V, 3, H, W)
-        d_depth = _c(np.zeros((B, V, 1, H, W)) if d_depth is None else d_depth).reshape(B, V, 1, H, W)
-        d_alpha = _c(np.zeros((B, V, 1, H, W)) if d_alpha is None else d_alpha).reshape(B, V, 1, H, W)
-        dg = np.zeros((B, N, 14), np.float32)
+        d_image = _c(d_image, dt).reshape(B, V, 3, H, W)
+        d_depth = _c(np.zeros((B, V, 1, H, W)) if d_depth is None else d_depth, dt).reshape(B, V, 1, H, W)
+        d_alpha = _c(np.zeros((B, V, 1, H, W)) if d_alpha is None else d_alpha, dt).reshape(B, V, 1, H, W)
+        dg = np.zeros((B, N, 14), dt)
     if nthreads <= 0:
         nthreads = min(os.cpu_count() or 1, B * V)
-    rc = lib().lgm_oracle_render_batch(B, V, N, _f(g), _f(views), _f(projs), float(tanfov), float(tanfov),
-                                       float(scale_modifier), _f(bgv), H, W, _f(color), _f(depth), _f(alpha),
-                                       stats.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), _f(d_image),
-                                       _f(d_depth), _f(d_alpha), _f(dg), int(nthreads))
+    fp = (lambda a: None if a is None else a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))) if f64 else _f
+    rc = lib(f64).lgm_oracle_render_batch(B, V, N, fp(g), fp(views), fp(projs), float(tanfov), float(tanfov),
+                                       float(scale_modifier), fp(bgv), H, W, fp(color), fp(depth), fp(alpha),
+                                       stats.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), fp(d_image),
+                                       fp(d_depth), fp(d_alpha), fp(dg), int(nthreads))
     if rc != 0:
         raise RuntimeError("oracle render failed")
     out = {"image": color, "depth": depth, "alpha": alpha, "K": int(stats[0]), "evals": int(stats[1])}

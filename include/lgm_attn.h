@@ -1,0 +1,48 @@
+/*
+ * lgm_attn.h -- C ABI of the multi-view attention kernels in liblgm_amd.so (lgm_amd/csrc/attention.hip).
+ *
+ * Replaces the xformers call of core/attention.py:74-84 (MemEffAttention.forward:
+ *     x = memory_efficient_attention(q, k, v, attn_bias=None)   with q, k, v = unbind(qkv.reshape(B, L, 3, H, D), 2))
+ * and the fp32 torch fallback core/attention.py:51-64 (Attention.forward: softmax(q k^T * scale) v), both reached
+ * from core/unet.py:35-49 (MVAttention: L = num_frames * h * w tokens). Its backward replaces autograd through
+ * the same op (xformers' memory_efficient_attention backward / the fallback's matmul + softmax backward).
+ *
+ * Tensors (device pointers, element type `dtype`):
+ *   q, k, v : rows of the packed qkv Linear output [B, L, 3, H, D]; q = base, k = base + H*D, v = base + 2*H*D;
+ *             token rows are ld_qkv elements apart (3*H*D when packed). Must be 16-byte aligned.
+ *   o       : [B, L, H, D] contiguous (xformers output layout, core/attention.py:79).
+ *   lse     : [B, H, L] fp32, natural-log row log-sum-exp of scale * q k^T (saved for the backward).
+ *   d_o     : [B, L, H, D] contiguous; dq/dk/dv: same layout as q/k/v with row stride ld_dqkv.
+ * D must be 32, 64 or 128 (LGM's UNet: 16 heads over 512 or 1024 channels -> D = 32 or 64); accumulation is fp32.
+ * All work is enqueued on `stream` (a hipStream_t, NULL = default stream); nothing synchronises.
+ */
+#ifndef LGM_ATTN_H
+#define LGM_ATTN_H
+#include <stddef.h>
+
+#include "lgm_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LGM_ATTN_F32 0
+#define LGM_ATTN_BF16 1
+#define LGM_ATTN_F16 2
+
+/* Bytes of device scratch lgm_attn_backward needs (the fp32 delta = rowsum(dO * O) buffer). */
+size_t lgm_attn_workspace_size(int dtype, int B, int L, int H);
+
+/* o = softmax(scale * q k^T) v per (batch, head); also writes lse. */
+int lgm_attn_forward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,
+                     const void *v, long long ld_qkv, void *o, float *lse, void *stream);
+
+/* dq, dk, dv of the forward above given d_o (o and lse from the forward). Overwrites dq/dk/dv. */
+int lgm_attn_backward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,
+                      const void *v, long long ld_qkv, const void *o, const float *lse, const void *d_o, void *dq,
+                      void *dk, void *dv, long long ld_dqkv, void *workspace, size_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

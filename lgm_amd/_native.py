@@ -26,9 +26,10 @@ SIGNATURES = {
                                     _c_float, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _vp, _vp]),
     "lgm_render_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_float,
                                      _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _vp]),
-    "lgm_attn_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                   _vp, _vp, _vp, _vp, _c_size, _vp]),
+    "lgm_attn_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
+                                  _vp]),
+    "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
+                                   _vp, _vp, _vp, _vp, _c_ll, _vp, _c_size, _vp]),
     "lgm_attn_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "lgm_render_debug_counters": (_c_int, [_vp]),
     "lgm_render_set_flags": (_c_int, [_c_int]),

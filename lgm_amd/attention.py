@@ -1,0 +1,165 @@
+"""Multi-view self-attention of LGM's UNet on the HIP flash-attention kernels (lgm_amd/csrc/attention.hip).
+
+Drop-in replacements, with the same constructors, submodules (so state_dicts load unchanged) and forward
+signatures as the reference:
+  * Attention / MemEffAttention -- core/attention.py:31-84. Both compute softmax(scale q k^T) v through the MFMA
+    kernels; the reference's xformers call (core/attention.py:74-84) and its fp32 torch fallback (:51-64) are the
+    same function;
+  * MVAttention -- core/unet.py:11-49 (GroupNorm, the [B*F, C, h, w] <-> [B, F*h*w, C] token reshape across the
+    F views, attention, residual * skip_scale).
+q, k and v are read in place from the packed qkv Linear output and dq/dk/dv are written back packed, so the
+reshape/unbind/permute of the reference costs no copies. fp32, bf16 and fp16 activations are supported (bf16 is
+what LGM trains with under accelerate's mixed precision); accumulation is fp32.
+No CPU path: CPU tensors raise (the xformers path of the reference is GPU-only too).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _native as nat
+
+_DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype not in _DTYPES:
+        raise nat.NativeError(f"attention supports float32/bfloat16/float16, got {t.dtype}")
+    return _DTYPES[t.dtype]
+
+
+class _PackedAttention(torch.autograd.Function):
+    """o = softmax(scale q k^T) v with q, k, v = qkv.unbind(2), qkv [B, L, 3, H, D] contiguous -> o [B, L, H, D]."""
+
+    @staticmethod
+    def forward(ctx, qkv: torch.Tensor, scale: float):
+        nat.require_device_tensor(qkv, "qkv")
+        qkv = qkv.contiguous()
+        B, L, three, H, D = qkv.shape
+        if three != 3:
+            raise nat.NativeError(f"qkv must be [B, L, 3, H, D], got {tuple(qkv.shape)}")
+        dt = _dtype_code(qkv)
+        o = torch.empty((B, L, H, D), device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty((B, H, L), device=qkv.device, dtype=torch.float32)
+        if B * L * H > 0:
+            base, es = qkv.data_ptr(), qkv.element_size()
+            L_ = nat.lib()
+            nat.check(L_.lgm_attn_forward(dt, B, L, H, D, float(scale), base, base + H * D * es,
+                                          base + 2 * H * D * es, 3 * H * D, nat.ptr(o), nat.ptr(lse),
+                                          nat.stream_of(qkv.device)), "lgm_attn_forward")
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.scale = float(scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, d_o: torch.Tensor):
+        qkv, o, lse = ctx.saved_tensors
+        B, L, _, H, D = qkv.shape
+        d_o = d_o.to(qkv.dtype).contiguous()
+        d_qkv = torch.empty_like(qkv)
+        if B * L * H > 0:
+            dt = _dtype_code(qkv)
+            L_ = nat.lib()
+            ws_bytes = L_.lgm_attn_workspace_size(dt, B, L, H)
+            ws = torch.empty(max(ws_bytes, 1), device=qkv.device, dtype=torch.uint8)
+            base, dbase, es = qkv.data_ptr(), d_qkv.data_ptr(), qkv.element_size()
+            hd = H * D * es
+            nat.check(L_.lgm_attn_backward(dt, B, L, H, D, ctx.scale, base, base + hd, base + 2 * hd, 3 * H * D,
+                                           nat.ptr(o), nat.ptr(lse), nat.ptr(d_o), dbase, dbase + hd,
+                                           dbase + 2 * hd, 3 * H * D, nat.ptr(ws), ws_bytes,
+                                           nat.stream_of(qkv.device)), "lgm_attn_backward")
+        return d_qkv, None
+
+
+def packed_attention(qkv: torch.Tensor, scale: float | None = None) -> torch.Tensor:
+    """qkv [B, L, 3, H, D] (the reshaped qkv Linear output) -> [B, L, H, D]; scale defaults to D^-1/2."""
+    if scale is None:
+        scale = qkv.shape[-1] ** -0.5
+    return _PackedAttention.apply(qkv, scale)
+
+
+def memory_efficient_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, attn_bias=None,
+                               scale: float | None = None) -> torch.Tensor:
+    """xformers.ops.memory_efficient_attention subset used by core/attention.py:79: q, k, v [B, L, H, D], no bias,
+    no dropout. Views of one packed [B, L, 3, H, D] tensor (what unbind(qkv, 2) yields) are used in place;
+    otherwise the three are stacked first."""
+    if attn_bias is not None:
+        raise NotImplementedError("attn_bias is not supported (LGM never passes one: core/unet.py:43)")
+    if not (q.shape == k.shape == v.shape) or q.dim() != 4:
+        raise ValueError("q, k, v must all be [B, L, H, D]")
+    B, L, H, D = q.shape
+    es = q.element_size()
+    packed = (q.dtype == k.dtype == v.dtype and q.stride() == k.stride() == v.stride()
+              and q.stride() == (L * 3 * H * D, 3 * H * D, D, 1)
+              and k.data_ptr() - q.data_ptr() == H * D * es and v.data_ptr() - q.data_ptr() == 2 * H * D * es)
+    if packed:
+        qkv = torch.as_strided(q, (B, L, 3, H, D), (L * 3 * H * D, 3 * H * D, H * D, D, 1))
+    else:
+        qkv = torch.stack([q, k, v], dim=2)
+    return packed_attention(qkv, scale)
+
+
+class Attention(nn.Module):
+    """core/attention.py:31-64 (same constructor and parameters)."""
+
+    def __init__(self, dim: int, num_heads: int = 8, qkv_bias: bool = False, proj_bias: bool = True,
+                 attn_drop: float = 0.0, proj_drop: float = 0.0) -> None:
+        super().__init__()
+        self.num_heads = num_heads
+        head_dim = dim // num_heads
+        self.scale = head_dim ** -0.5
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim, bias=proj_bias)
+        self.proj_drop = nn.Dropout(proj_drop)
+
+    def _attend(self, x: torch.Tensor) -> torch.Tensor:
+        if self.training and self.attn_drop.p > 0:
+            raise NotImplementedError("attention-probability dropout is not implemented (LGM uses attn_drop=0)")
+        B, N, C = x.shape
+        qkv = self.qkv(x).reshape(B, N, 3, self.num_heads, C // self.num_heads)
+        y = packed_attention(qkv, self.scale).reshape(B, N, C)
+        return self.proj_drop(self.proj(y))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self._attend(x)
+
+
+class MemEffAttention(Attention):
+    """core/attention.py:67-84."""
+
+    def forward(self, x: torch.Tensor, attn_bias=None) -> torch.Tensor:
+        if attn_bias is not None:
+            raise AssertionError("attn_bias (nested tensors) is not supported")
+        return self._attend(x)
+
+
+class MVAttention(nn.Module):
+    """core/unet.py:11-49: self-attention across the tokens of all `num_frames` views of an object.
+
+    num_frames defaults to 4 like the reference (whose UNet never overrides it, core/unet.py:24 'hardcoded');
+    here it is a real parameter."""
+
+    def __init__(self, dim: int, num_heads: int = 8, qkv_bias: bool = False, proj_bias: bool = True,
+                 attn_drop: float = 0.0, proj_drop: float = 0.0, groups: int = 32, eps: float = 1e-5,
+                 residual: bool = True, skip_scale: float = 1, num_frames: int = 4):
+        super().__init__()
+        self.residual = residual
+        self.skip_scale = skip_scale
+        self.num_frames = num_frames
+        self.norm = nn.GroupNorm(num_groups=groups, num_channels=dim, eps=eps, affine=True)
+        self.attn = MemEffAttention(dim, num_heads, qkv_bias, proj_bias, attn_drop, proj_drop)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        BV, C, H, W = x.shape
+        if BV % self.num_frames:
+            raise ValueError(f"batch {BV} is not a multiple of num_frames={self.num_frames}")
+        B = BV // self.num_frames
+        res = x
+        x = self.norm(x)
+        x = x.reshape(B, self.num_frames, C, H, W).permute(0, 1, 3, 4, 2).reshape(B, -1, C)
+        x = self.attn(x)
+        x = x.reshape(B, self.num_frames, H, W, C).permute(0, 1, 4, 2, 3).reshape(BV, C, H, W)
+        if self.residual:
+            x = (x + res) * self.skip_scale
+        return x

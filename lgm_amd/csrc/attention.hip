@@ -1,0 +1,488 @@
+// lgm_amd/csrc/attention.hip -- MFMA flash attention (forward + backward) for LGM's multi-view self-attention.
+//
+// Replaces xformers.ops.memory_efficient_attention as called by core/attention.py:74-84 (MemEffAttention, used by
+// core/unet.py:35-49 MVAttention), and its pure-torch fallback core/attention.py:51-64:
+//     out = softmax(scale * q k^T) v,  q, k, v in xformers layout [B, L, H, D], scale = D^-1/2, no bias, p = 0.
+// q/k/v are read in place from the packed qkv Linear output [B, L, 3, H, D] (row stride ld = 3 H D elements), so
+// the reshape/unbind of core/attention.py:75-77 costs nothing; dq/dk/dv are written back packed the same way.
+//
+// Design (CDNA4, wave64, 16x16 MFMA tiles; fp32 accumulation):
+//   * scores are computed TRANSPOSED, S^T = K Q^T, so every lane owns one query column (q = lane & 15) and holds
+//     4 keys of each 16-key sub-tile: the online-softmax row state (m, l) and the O^T accumulator live in the
+//     same lane, and the P tile feeds the P V product from registers (its key order permuted to match the
+//     accumulator layout; the matching V^T operand is read with the same permutation from LDS);
+//   * bf16 / fp16 use v_mfma_f32_16x16x32_{bf16,f16}; fp32 uses the exact-f32 v_mfma_f32_16x16x4_f32, so fp32
+//     inputs keep the fp32 accuracy of the reference's fallback;
+//   * the softmax runs in base 2 (exp2 with a log2(e) prescale); LSE is stored in natural log for the backward;
+//   * backward = delta = rowsum(dO * O), then a dQ kernel (per query block, loops over key blocks) and a dK/dV
+//     kernel (per key block, loops over query blocks): no atomics, deterministic.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "common.h"
+#include "lgm_attn.h"
+
+namespace lgm {
+namespace attn {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+constexpr int BQ = 64, BK = 64, NT = 256;  // 4 wavefronts x 16 rows
+
+template <int DT> struct Ty;
+template <> struct Ty<LGM_ATTN_F32> { using T = float; static constexpr int PAD = 2; };
+template <> struct Ty<LGM_ATTN_BF16> { using T = __bf16; using V8 = bf16x8; static constexpr int PAD = 8; };
+template <> struct Ty<LGM_ATTN_F16> { using T = _Float16; using V8 = f16x8; static constexpr int PAD = 8; };
+constexpr int PADT = 4;  // transposed bf16/fp16 tiles: [D][64 + 4]
+
+template <typename T> __device__ __forceinline__ float to_f(T x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x) { return (T)x; }
+
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+template <int DT> __device__ __forceinline__ f32x4 mfma32(typename Ty<DT>::V8 a, typename Ty<DT>::V8 b, f32x4 c) {
+    if constexpr (DT == LGM_ATTN_BF16) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// Register fragment of a 16-row operand Y[row = lane & 15][0..D): fp32 -> D/4 values Y[r][4s + g];
+// 16-bit -> D/32 vectors Y[r][32c + 8g + 0..7].
+template <int DT, int D> struct YFrag;
+template <int D> struct YFrag<LGM_ATTN_F32, D> { float v[D / 4]; };
+template <int D> struct YFrag<LGM_ATTN_BF16, D> { bf16x8 v[D / 32]; };
+template <int D> struct YFrag<LGM_ATTN_F16, D> { f16x8 v[D / 32]; };
+
+template <int DT, int D>
+__device__ __forceinline__ void load_yfrag(YFrag<DT, D> &f, const typename Ty<DT>::T *row, bool valid, int g) {
+    using T = typename Ty<DT>::T;
+    if constexpr (DT == LGM_ATTN_F32) {
+#pragma unroll
+        for (int s = 0; s < D / 4; s++) f.v[s] = valid ? row[4 * s + g] : 0.f;
+    } else {
+        using V8 = typename Ty<DT>::V8;
+#pragma unroll
+        for (int c = 0; c < D / 32; c++) {
+            if (valid) f.v[c] = *reinterpret_cast<const V8 *>(row + 32 * c + 8 * g);
+            else
+#pragma unroll
+                for (int j = 0; j < 8; j++) f.v[c][j] = (T)0.f;
+        }
+    }
+}
+
+// acc[i] += (X Y^T)[rb + 4g + i][lane & 15]: X rows from an LDS row-major tile (stride ldx), Y = register frag.
+template <int DT, int D>
+__device__ __forceinline__ void s_like(f32x4 &acc, const typename Ty<DT>::T *X, int ldx, int rb,
+                                       const YFrag<DT, D> &y, int g, int r16) {
+    const typename Ty<DT>::T *xr = X + (rb + r16) * ldx;
+    if constexpr (DT == LGM_ATTN_F32) {
+#pragma unroll
+        for (int s = 0; s < D / 4; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * s + g], y.v[s], acc, 0, 0, 0);
+    } else {
+        using V8 = typename Ty<DT>::V8;
+#pragma unroll
+        for (int c = 0; c < D / 32; c++)
+            acc = mfma32<DT>(*reinterpret_cast<const V8 *>(xr + 32 * c + 8 * g), y.v[c], acc);
+    }
+}
+
+// acc[dt][i] += (Z^T P)[d = 16 dt + 4g + i][col = lane & 15] over the 64 keys of a block, where P is held by the
+// lanes as own[sub][i] = P[key = 16 sub + 4g + i][col]. fp32: Z is the row-major LDS tile [key][d] (stride ldz);
+// 16-bit: Zt is the TRANSPOSED LDS tile [d][key] (stride ldzt), read with the key permutation of the operand.
+template <int DT, int D>
+__device__ __forceinline__ void pv_like(f32x4 (&acc)[D / 16], const typename Ty<DT>::T *Z, int ldz,
+                                        const float (&own)[4][4], int g, int r16) {
+    if constexpr (DT == LGM_ATTN_F32) {
+#pragma unroll
+        for (int dt = 0; dt < D / 16; dt++)
+#pragma unroll
+            for (int sub = 0; sub < 4; sub++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    acc[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Z[(16 * sub + 4 * g + i) * ldz + 16 * dt + r16],
+                                                                    own[sub][i], acc[dt], 0, 0, 0);
+    } else {
+        using T = typename Ty<DT>::T;
+        using V8 = typename Ty<DT>::V8;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            V8 b;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                b[i] = (T)own[2 * t][i];
+                b[4 + i] = (T)own[2 * t + 1][i];
+            }
+#pragma unroll
+            for (int dt = 0; dt < D / 16; dt++) {
+                const T *zr = Z + (16 * dt + r16) * ldz + 32 * t + 4 * g;
+                const uint2 lo = *reinterpret_cast<const uint2 *>(zr);
+                const uint2 hi = *reinterpret_cast<const uint2 *>(zr + 16);
+                V8 a;
+                const uint4 packed = make_uint4(lo.x, lo.y, hi.x, hi.y);
+                a = *reinterpret_cast<const V8 *>(&packed);
+                acc[dt] = mfma32<DT>(a, b, acc[dt]);
+            }
+        }
+    }
+}
+
+// Cooperative loads of a 64-row block (rows r0.., tokens >= L zero-filled) from a [tokens][ld] tensor.
+template <typename T, int D, int PAD>
+__device__ __forceinline__ void load_rows(T *dst, const T *src, long long ld, int r0, int L) {
+    constexpr int VEC = 16 / sizeof(T), CPR = D / VEC;
+    for (int c = threadIdx.x; c < 64 * CPR; c += NT) {
+        const int r = c / CPR, col = (c - r * CPR) * VEC;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (r0 + r < L) v = *reinterpret_cast<const uint4 *>(src + (long long)(r0 + r) * ld + col);
+        if constexpr (PAD % VEC == 0) {
+            *reinterpret_cast<uint4 *>(dst + r * (D + PAD) + col) = v;
+        } else {
+            const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+            for (int j = 0; j < VEC; j++) dst[r * (D + PAD) + col + j] = pv[j];
+        }
+    }
+}
+template <typename T, int D>
+__device__ __forceinline__ void load_rows_T(T *dst, const T *src, long long ld, int r0, int L) {
+    constexpr int VEC = 16 / sizeof(T), CPR = D / VEC;
+    for (int c = threadIdx.x; c < 64 * CPR; c += NT) {
+        const int r = c / CPR, col = (c - r * CPR) * VEC;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (r0 + r < L) v = *reinterpret_cast<const uint4 *>(src + (long long)(r0 + r) * ld + col);
+        const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+        for (int j = 0; j < VEC; j++) dst[(col + j) * (64 + PADT) + r] = pv[j];
+    }
+}
+
+__device__ __forceinline__ float xmax4(float v) {
+    v = fmaxf(v, __shfl_xor(v, 16, 64));
+    return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float xsum4(float v) {
+    v += __shfl_xor(v, 16, 64);
+    return v + __shfl_xor(v, 32, 64);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// forward: grid (ceil(L/64), B*H), block 256.
+template <int DT, int D>
+__global__ __launch_bounds__(NT) void k_attn_fwd(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+                                                 const typename Ty<DT>::T *__restrict__ k,
+                                                 const typename Ty<DT>::T *__restrict__ v, long long ld,
+                                                 typename Ty<DT>::T *__restrict__ o, float *__restrict__ lse) {
+    using T = typename Ty<DT>::T;
+    constexpr int PAD = Ty<DT>::PAD;
+    constexpr bool F32 = DT == LGM_ATTN_F32;
+    __shared__ __attribute__((aligned(16))) T Ks[64 * (D + PAD)];
+    __shared__ __attribute__((aligned(16))) T Vs[F32 ? 64 * (D + PAD) : D * (64 + PADT)];
+    const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+    const long long base = (long long)b * L * ld + (long long)h * D;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
+    const int qrow = blockIdx.x * BQ + w * 16 + r16;
+    const bool qvalid = qrow < L;
+    const float c = scale * LOG2E;
+    YFrag<DT, D> qf;
+    load_yfrag<DT, D>(qf, q + base + (long long)qrow * ld, qvalid, g);
+    f32x4 oacc[D / 16];
+#pragma unroll
+    for (int dt = 0; dt < D / 16; dt++) oacc[dt] = zero4();
+    float m = -INFINITY, lsum = 0.f;
+    for (int kb = 0; kb < L; kb += BK) {
+        __syncthreads();
+        load_rows<T, D, PAD>(Ks, k + base, ld, kb, L);
+        if constexpr (F32) load_rows<T, D, PAD>(Vs, v + base, ld, kb, L);
+        else load_rows_T<T, D>(Vs, v + base, ld, kb, L);
+        __syncthreads();
+        float p[4][4];
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int sub = 0; sub < 4; sub++) {
+            f32x4 s = zero4();
+            s_like<DT, D>(s, Ks, D + PAD, 16 * sub, qf, g, r16);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const float x = (kb + 16 * sub + 4 * g + i < L) ? s[i] * c : -INFINITY;
+                p[sub][i] = x;
+                mloc = fmaxf(mloc, x);
+            }
+        }
+        mloc = xmax4(mloc);
+        const float mnew = fmaxf(m, mloc);
+        const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m - mnew);
+        float ls = 0.f;
+#pragma unroll
+        for (int sub = 0; sub < 4; sub++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const float e = (mnew == -INFINITY) ? 0.f : exp2f(p[sub][i] - mnew);
+                p[sub][i] = e;
+                ls += e;
+            }
+        lsum = lsum * alpha + xsum4(ls);
+#pragma unroll
+        for (int dt = 0; dt < D / 16; dt++) oacc[dt] *= alpha;
+        pv_like<DT, D>(oacc, Vs, F32 ? D + PAD : 64 + PADT, p, g, r16);
+        m = mnew;
+    }
+    if (qvalid) {
+        const float inv = 1.f / lsum;
+        T *orow = o + ((long long)b * L + qrow) * ((long long)H * D) + (long long)h * D;
+#pragma unroll
+        for (int dt = 0; dt < D / 16; dt++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) orow[16 * dt + 4 * g + i] = from_f<T>(oacc[dt][i] * inv);
+        if (g == 0) lse[(long long)bh * L + qrow] = (m + log2f(lsum)) * LN2;
+    }
+}
+
+// delta[bh][q] = sum_d dO[q][d] * O[q][d]  (fp32); grid ceil(B*L*H / 256).
+template <int DT, int D>
+__global__ __launch_bounds__(256) void k_attn_delta(int B, int L, int H, const typename Ty<DT>::T *__restrict__ o,
+                                                    const typename Ty<DT>::T *__restrict__ dout,
+                                                    float *__restrict__ delta) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;  // (b, q, h)
+    if (idx >= (long long)B * L * H) return;
+    const long long bq = idx / H;
+    const int h = (int)(idx - bq * H);
+    const int b = (int)(bq / L), qrow = (int)(bq - (long long)b * L);
+    const long long off = idx * D;
+    float s = 0.f;
+#pragma unroll 8
+    for (int d = 0; d < D; d++) s += to_f(o[off + d]) * to_f(dout[off + d]);
+    delta[((long long)b * H + h) * L + qrow] = s;
+}
+
+// dQ: grid (ceil(L/64), B*H). dQ = scale * sum_k dS K with dS = P o (dP - delta), P = exp(scale S - lse).
+template <int DT, int D>
+__global__ __launch_bounds__(NT) void k_attn_dq(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+                                                const typename Ty<DT>::T *__restrict__ k,
+                                                const typename Ty<DT>::T *__restrict__ v, long long ld,
+                                                const typename Ty<DT>::T *__restrict__ dout,
+                                                const float *__restrict__ lse, const float *__restrict__ delta,
+                                                typename Ty<DT>::T *__restrict__ dq, long long ldd) {
+    using T = typename Ty<DT>::T;
+    constexpr int PAD = Ty<DT>::PAD;
+    constexpr bool F32 = DT == LGM_ATTN_F32;
+    __shared__ __attribute__((aligned(16))) T Ks[64 * (D + PAD)];
+    __shared__ __attribute__((aligned(16))) T Vs[64 * (D + PAD)];
+    __shared__ __attribute__((aligned(16))) T Kt[F32 ? 1 : D * (64 + PADT)];
+    const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+    const long long base = (long long)b * L * ld + (long long)h * D;
+    const long long obase = (long long)b * L * H * D + (long long)h * D;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
+    const int qrow = blockIdx.x * BQ + w * 16 + r16;
+    const bool qvalid = qrow < L;
+    const float c = scale * LOG2E;
+    YFrag<DT, D> qf, dof;
+    load_yfrag<DT, D>(qf, q + base + (long long)qrow * ld, qvalid, g);
+    load_yfrag<DT, D>(dof, dout + obase + (long long)qrow * H * D, qvalid, g);
+    const float lse2 = qvalid ? lse[(long long)bh * L + qrow] * LOG2E : 0.f;
+    const float dlt = qvalid ? delta[(long long)bh * L + qrow] : 0.f;
+    f32x4 acc[D / 16];
+#pragma unroll
+    for (int dt = 0; dt < D / 16; dt++) acc[dt] = zero4();
+    for (int kb = 0; kb < L; kb += BK) {
+        __syncthreads();
+        load_rows<T, D, PAD>(Ks, k + base, ld, kb, L);
+        load_rows<T, D, PAD>(Vs, v + base, ld, kb, L);
+        if constexpr (!F32) load_rows_T<T, D>(Kt, k + base, ld, kb, L);
+        __syncthreads();
+        float ds[4][4];
+#pragma unroll
+        for (int sub = 0; sub < 4; sub++) {
+            f32x4 s = zero4(), dp = zero4();
+            s_like<DT, D>(s, Ks, D + PAD, 16 * sub, qf, g, r16);
+            s_like<DT, D>(dp, Vs, D + PAD, 16 * sub, dof, g, r16);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const bool kv = kb + 16 * sub + 4 * g + i < L;
+                const float p = (kv && qvalid) ? exp2f(s[i] * c - lse2) : 0.f;
+                ds[sub][i] = p * (dp[i] - dlt);
+            }
+        }
+        pv_like<DT, D>(acc, F32 ? Ks : Kt, F32 ? D + PAD : 64 + PADT, ds, g, r16);
+    }
+    if (qvalid) {
+        T *row = dq + (long long)b * L * ldd + (long long)qrow * ldd + (long long)h * D;
+#pragma unroll
+        for (int dt = 0; dt < D / 16; dt++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) row[16 * dt + 4 * g + i] = from_f<T>(acc[dt][i] * scale);
+    }
+}
+
+// dK, dV: grid (ceil(L/64), B*H); each wavefront owns 16 keys, loops over all query blocks.
+template <int DT, int D>
+__global__ __launch_bounds__(NT) void k_attn_dkdv(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+                                                  const typename Ty<DT>::T *__restrict__ k,
+                                                  const typename Ty<DT>::T *__restrict__ v, long long ld,
+                                                  const typename Ty<DT>::T *__restrict__ dout,
+                                                  const float *__restrict__ lse, const float *__restrict__ delta,
+                                                  typename Ty<DT>::T *__restrict__ dk, typename Ty<DT>::T *__restrict__ dv,
+                                                  long long ldd) {
+    using T = typename Ty<DT>::T;
+    constexpr int PAD = Ty<DT>::PAD;
+    constexpr bool F32 = DT == LGM_ATTN_F32;
+    __shared__ __attribute__((aligned(16))) T Qs[64 * (D + PAD)];
+    __shared__ __attribute__((aligned(16))) T Os[64 * (D + PAD)];  // dO rows
+    __shared__ __attribute__((aligned(16))) T Qt[F32 ? 1 : D * (64 + PADT)];
+    __shared__ __attribute__((aligned(16))) T Ot[F32 ? 1 : D * (64 + PADT)];
+    __shared__ float sl[64], sd[64];
+    const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+    const long long base = (long long)b * L * ld + (long long)h * D;
+    const long long obase = (long long)b * L * H * D + (long long)h * D;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
+    const int key = blockIdx.x * BK + w * 16 + r16;
+    const bool kvalid = key < L;
+    const float c = scale * LOG2E;
+    YFrag<DT, D> kf, vf;
+    load_yfrag<DT, D>(kf, k + base + (long long)key * ld, kvalid, g);
+    load_yfrag<DT, D>(vf, v + base + (long long)key * ld, kvalid, g);
+    f32x4 dka[D / 16], dva[D / 16];
+#pragma unroll
+    for (int dt = 0; dt < D / 16; dt++) { dka[dt] = zero4(); dva[dt] = zero4(); }
+    for (int qb = 0; qb < L; qb += BQ) {
+        __syncthreads();
+        load_rows<T, D, PAD>(Qs, q + base, ld, qb, L);
+        load_rows<T, D, PAD>(Os, dout + obase, (long long)H * D, qb, L);
+        if constexpr (!F32) {
+            load_rows_T<T, D>(Qt, q + base, ld, qb, L);
+            load_rows_T<T, D>(Ot, dout + obase, (long long)H * D, qb, L);
+        }
+        if (tid < 64) {
+            const bool qv = qb + tid < L;
+            sl[tid] = qv ? lse[(long long)bh * L + qb + tid] * LOG2E : INFINITY;  // invalid rows: P = 0
+            sd[tid] = qv ? delta[(long long)bh * L + qb + tid] : 0.f;
+        }
+        __syncthreads();
+        float p[4][4], ds[4][4];
+#pragma unroll
+        for (int sub = 0; sub < 4; sub++) {
+            f32x4 s = zero4(), dp = zero4();
+            s_like<DT, D>(s, Qs, D + PAD, 16 * sub, kf, g, r16);   // S[q = 16 sub + 4g + i][key]
+            s_like<DT, D>(dp, Os, D + PAD, 16 * sub, vf, g, r16);  // dP[q][key]
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int qi = 16 * sub + 4 * g + i;
+                const float e = exp2f(s[i] * c - sl[qi]);
+                p[sub][i] = e;
+                ds[sub][i] = e * (dp[i] - sd[qi]);
+            }
+        }
+        pv_like<DT, D>(dva, F32 ? Os : Ot, F32 ? D + PAD : 64 + PADT, p, g, r16);   // dV^T += dO^T P
+        pv_like<DT, D>(dka, F32 ? Qs : Qt, F32 ? D + PAD : 64 + PADT, ds, g, r16);  // dK^T += Q^T dS
+    }
+    if (kvalid) {
+        T *krow = dk + (long long)b * L * ldd + (long long)key * ldd + (long long)h * D;
+        T *vrow = dv + (long long)b * L * ldd + (long long)key * ldd + (long long)h * D;
+#pragma unroll
+        for (int dt = 0; dt < D / 16; dt++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                krow[16 * dt + 4 * g + i] = from_f<T>(dka[dt][i] * scale);
+                vrow[16 * dt + 4 * g + i] = from_f<T>(dva[dt][i]);
+            }
+    }
+}
+
+template <int DT, int D>
+int fwd_impl(int B, int L, int H, float scale, const void *q, const void *k, const void *v, long long ld, void *o,
+             float *lse, hipStream_t st) {
+    using T = typename Ty<DT>::T;
+    dim3 grid((L + BQ - 1) / BQ, B * H);
+    LGM_LAUNCH("k_attn_fwd", st, (k_attn_fwd<DT, D><<<grid, NT, 0, st>>>(L, H, scale, (const T *)q, (const T *)k,
+                                                                       (const T *)v, ld, (T *)o, lse)));
+    return LGM_OK;
+}
+
+template <int DT, int D>
+int bwd_impl(int B, int L, int H, float scale, const void *q, const void *k, const void *v, long long ld,
+             const void *o, const float *lse, const void *dout, void *dq, void *dk, void *dv, long long ldd,
+             float *delta, hipStream_t st) {
+    using T = typename Ty<DT>::T;
+    const long long rows = (long long)B * L * H;
+    LGM_LAUNCH("k_attn_delta", st, (k_attn_delta<DT, D><<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(
+                                       B, L, H, (const T *)o, (const T *)dout, delta)));
+    dim3 grid((L + 63) / 64, B * H);
+    LGM_LAUNCH("k_attn_dq", st, (k_attn_dq<DT, D><<<grid, NT, 0, st>>>(L, H, scale, (const T *)q, (const T *)k,
+                                                                     (const T *)v, ld, (const T *)dout, lse, delta,
+                                                                     (T *)dq, ldd)));
+    LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv<DT, D><<<grid, NT, 0, st>>>(L, H, scale, (const T *)q, (const T *)k,
+                                                                         (const T *)v, ld, (const T *)dout, lse,
+                                                                         delta, (T *)dk, (T *)dv, ldd)));
+    return LGM_OK;
+}
+
+int check(int dtype, int B, int L, int H, int D) {
+    if (dtype < 0 || dtype > 2 || B <= 0 || L <= 0 || H <= 0 || !(D == 32 || D == 64 || D == 128)) {
+        set_error("unsupported attention shape/dtype (dtype=%d B=%d L=%d H=%d D=%d; D must be 32, 64 or 128)", dtype,
+                  B, L, H, D);
+        return LGM_E_INVALID;
+    }
+    return LGM_OK;
+}
+
+}  // namespace attn
+}  // namespace lgm
+
+#define LGM_ATTN_DISPATCH(FN, ...)                                                                             \
+    switch (dtype * 1000 + D) {                                                                                \
+        case LGM_ATTN_F32 * 1000 + 32: return lgm::attn::FN<LGM_ATTN_F32, 32>(__VA_ARGS__);                   \
+        case LGM_ATTN_F32 * 1000 + 64: return lgm::attn::FN<LGM_ATTN_F32, 64>(__VA_ARGS__);                   \
+        case LGM_ATTN_F32 * 1000 + 128: return lgm::attn::FN<LGM_ATTN_F32, 128>(__VA_ARGS__);                 \
+        case LGM_ATTN_BF16 * 1000 + 32: return lgm::attn::FN<LGM_ATTN_BF16, 32>(__VA_ARGS__);                 \
+        case LGM_ATTN_BF16 * 1000 + 64: return lgm::attn::FN<LGM_ATTN_BF16, 64>(__VA_ARGS__);                 \
+        case LGM_ATTN_BF16 * 1000 + 128: return lgm::attn::FN<LGM_ATTN_BF16, 128>(__VA_ARGS__);               \
+        case LGM_ATTN_F16 * 1000 + 32: return lgm::attn::FN<LGM_ATTN_F16, 32>(__VA_ARGS__);                   \
+        case LGM_ATTN_F16 * 1000 + 64: return lgm::attn::FN<LGM_ATTN_F16, 64>(__VA_ARGS__);                   \
+        case LGM_ATTN_F16 * 1000 + 128: return lgm::attn::FN<LGM_ATTN_F16, 128>(__VA_ARGS__);                 \
+        default: return LGM_E_INVALID;                                                                         \
+    }
+
+extern "C" {
+
+size_t lgm_attn_workspace_size(int dtype, int B, int L, int H) {
+    if (B <= 0 || L <= 0 || H <= 0) return 0;
+    return (size_t)B * L * H * sizeof(float);  // delta
+}
+
+int lgm_attn_forward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,
+                     const void *v, long long ld_qkv, void *o, float *lse, void *stream) {
+    lgm::clear_error();
+    int rc = lgm::attn::check(dtype, B, L, H, D);
+    if (rc) return rc;
+    if (!q || !k || !v || !o || !lse) {
+        lgm::set_error("null pointer");
+        return LGM_E_INVALID;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    LGM_ATTN_DISPATCH(fwd_impl, B, L, H, scale, q, k, v, ld_qkv, o, lse, st)
+}
+
+int lgm_attn_backward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,
+                      const void *v, long long ld_qkv, const void *o, const float *lse, const void *d_o, void *dq,
+                      void *dk, void *dv, long long ld_dqkv, void *workspace, size_t workspace_bytes, void *stream) {
+    lgm::clear_error();
+    int rc = lgm::attn::check(dtype, B, L, H, D);
+    if (rc) return rc;
+    if (!q || !k || !v || !o || !lse || !d_o || !dq || !dk || !dv) {
+        lgm::set_error("null pointer");
+        return LGM_E_INVALID;
+    }
+    if (!workspace || workspace_bytes < lgm_attn_workspace_size(dtype, B, L, H)) {
+        lgm::set_error("attention workspace too small");
+        return LGM_E_WORKSPACE;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    LGM_ATTN_DISPATCH(bwd_impl, B, L, H, scale, q, k, v, ld_qkv, o, lse, d_o, dq, dk, dv, ld_dqkv,
+                      (float *)workspace, st)
+}
+
+}  // extern "C"

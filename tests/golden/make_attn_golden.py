@@ -1,0 +1,64 @@
+"""Golden vectors for the attention path, produced by the REFERENCE's own modules (run in the survey container
+only; /root/reference never travels): core/attention.py MemEffAttention (pure-torch fallback, XFORMERS_DISABLED=1:
+core/attention.py:16-28, 51-64) and core/unet.py MVAttention (:11-49). fp32, CPU.
+
+Each case stores: x, upstream grad gy, the module's state_dict (same parameter names as ours), y, dx, and the
+parameter gradients. Regenerate with: PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_attn_golden.py
+"""
+import os
+import sys
+import zlib
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+
+
+def main():
+    os.environ["XFORMERS_DISABLED"] = "1"
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    from core.attention import MemEffAttention  # noqa: E402  (reference code, read-only)
+    from core.unet import MVAttention  # noqa: E402
+
+    torch.manual_seed(0)
+    # LGM's head dims are 32 (C=512 / 16 heads) and 64 (C=1024 / 16 heads); channel counts are reduced here to
+    # keep the fixtures small, token counts L = F*h*w keep LGM's structure (incl. L = 600, not a multiple of 64).
+    cases = [
+        # name, kind, ctor kwargs, input shape
+        ("memeff_d128_h4", "memeff", dict(dim=128, num_heads=4), (2, 200, 128)),
+        ("memeff_d128_h2", "memeff", dict(dim=128, num_heads=2), (1, 130, 128)),
+        ("mv_c64_h2_f4", "mv", dict(dim=64, num_heads=2, num_frames=4, skip_scale=0.5 ** 0.5), (4, 64, 4, 4)),
+        ("mv_c128_h4_f4", "mv", dict(dim=128, num_heads=4, num_frames=4, skip_scale=0.5 ** 0.5), (4, 128, 16, 16)),
+        ("mv_c256_h4_f4", "mv", dict(dim=256, num_heads=4, num_frames=4, skip_scale=0.5 ** 0.5), (4, 256, 8, 8)),
+        ("mv_c128_h4_f6", "mv", dict(dim=128, num_heads=4, num_frames=6, skip_scale=0.5 ** 0.5), (6, 128, 10, 10)),
+    ]
+    for name, kind, kw, shape in cases:
+        g = torch.Generator().manual_seed(zlib.crc32(name.encode()))
+        if kind == "memeff":
+            m = MemEffAttention(kw["dim"], kw["num_heads"], qkv_bias=False, proj_bias=True)
+        else:
+            m = MVAttention(kw["dim"], kw["num_heads"], num_frames=kw["num_frames"], skip_scale=kw["skip_scale"])
+        with torch.no_grad():
+            for p in m.parameters():
+                p.copy_(torch.randn(p.shape, generator=g) * (0.5 / np.sqrt(p.shape[-1]) if p.dim() > 1 else 0.1))
+            if kind == "mv":  # non-trivial GroupNorm affine
+                m.norm.weight.add_(1.0)
+        x = torch.randn(shape, generator=g, requires_grad=True)
+        y = m(x)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy)
+        out = {"x": x.detach().numpy(), "gy": gy.numpy(), "y": y.detach().numpy(), "dx": x.grad.numpy()}
+        for k, v in m.state_dict().items():
+            out["param." + k] = v.numpy()
+        for k, p in m.named_parameters():
+            out["grad." + k] = p.grad.numpy()
+        meta = dict(kind=kind, **kw)
+        np.savez_compressed(os.path.join(HERE, f"attn_{name}.npz"), meta=np.array(repr(meta)), **out)
+        print(name, {k: v.shape for k, v in out.items() if not k.startswith("param")})
+
+
+if __name__ == "__main__":
+    main()

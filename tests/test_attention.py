@@ -1,0 +1,180 @@
+"""Multi-view attention: oracle pinned to the reference's own modules (tests/golden/attn_*.npz, made by
+tests/golden/make_attn_golden.py from core/attention.py + core/unet.py), and the HIP flash-attention path
+(lgm_amd/attention.py -> lgm_attn_* in liblgm_amd.so) checked against them on the GPU.
+
+Tolerances: fp32 inputs -> 1e-4 relative L2 against the reference (the north_star bar; the exact-f32 MFMA path
+lands around 1e-6). bf16 / fp16 compute is compared with the fp64 result of the same rounded inputs:
+bf16 2e-2, fp16 3e-3 relative L2 (P and dS are rounded to the 8-/11-bit mantissa before the second MFMA).
+"""
+import ast
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import attention_ref as ref
+from render_cases import rel_l2
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "attn_*.npz")))
+
+
+def _load(path):
+    z = np.load(path)  # allow_pickle=False (default): plain arrays only
+    meta = ast.literal_eval(str(z["meta"]))
+    params = {k[6:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param.")}
+    grads = {k[5:]: z[k] for k in z.files if k.startswith("grad.")}
+    return meta, z, params, grads
+
+
+def _oracle_fn(meta, params):
+    if meta["kind"] == "memeff":
+        return lambda x, p: ref.attention(x, p, meta["num_heads"])
+    return lambda x, p: ref.mv_attention(x, p, meta["num_heads"], meta["num_frames"], meta["skip_scale"])
+
+
+def _module(meta):
+    from lgm_amd.attention import MemEffAttention, MVAttention
+    if meta["kind"] == "memeff":
+        return MemEffAttention(meta["dim"], meta["num_heads"], qkv_bias=False, proj_bias=True)
+    return MVAttention(meta["dim"], meta["num_heads"], num_frames=meta["num_frames"], skip_scale=meta["skip_scale"])
+
+
+def test_golden_present():
+    assert len(GOLDEN) >= 6
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=lambda p: os.path.basename(p)[5:-4])
+def test_oracle_reproduces_reference(path):
+    """The fp32 restatement reproduces the reference modules' outputs and gradients."""
+    meta, z, params, grads = _load(path)
+    p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    x = torch.from_numpy(z["x"]).requires_grad_(True)
+    y = _oracle_fn(meta, params)(x, p)
+    y.backward(torch.from_numpy(z["gy"]))
+    assert rel_l2(y.detach().numpy(), z["y"]) < 1e-6
+    assert rel_l2(x.grad.numpy(), z["dx"]) < 1e-5
+    for k, g in grads.items():
+        assert rel_l2(p[k].grad.numpy(), g) < 1e-5, k
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=lambda p: os.path.basename(p)[5:-4])
+def test_state_dict_compatible(path):
+    """Same submodule / parameter names and shapes as the reference module: its state_dict loads strictly."""
+    meta, z, params, _ = _load(path)
+    m = _module(meta)
+    m.load_state_dict(params, strict=True)
+
+
+def test_cpu_tensor_fails_loudly():
+    from lgm_amd import _native
+    from lgm_amd.attention import MemEffAttention
+    m = MemEffAttention(64, 2)
+    with pytest.raises(_native.NativeError):
+        m(torch.randn(1, 8, 64))
+
+
+# ------------------------------------------------------------------------------------------------------------ GPU
+def _packed_truth(qkv, scale, d_o):
+    """fp64 softmax attention and its gradient wrt packed qkv [B, L, 3, H, D]."""
+    x = qkv.detach().double().requires_grad_(True)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    o = ref.attention_core(q, k, v, scale).transpose(1, 2)
+    o.backward(d_o.double())
+    return o.detach(), x.grad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", GOLDEN, ids=lambda p: os.path.basename(p)[5:-4])
+def test_module_matches_reference_fp32(cuda, path):
+    meta, z, params, grads = _load(path)
+    m = _module(meta).to(cuda)
+    m.load_state_dict(params, strict=True)
+    x = torch.from_numpy(z["x"]).to(cuda).requires_grad_(True)
+    y = m(x)
+    y.backward(torch.from_numpy(z["gy"]).to(cuda))
+    torch.cuda.synchronize()
+    assert rel_l2(y.detach().cpu().numpy(), z["y"]) < 1e-4
+    assert rel_l2(x.grad.cpu().numpy(), z["dx"]) < 1e-4
+    named = dict(m.named_parameters())
+    for k, g in grads.items():
+        assert rel_l2(named[k].grad.cpu().numpy(), g) < 1e-4, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", [p for p in GOLDEN if "_mv_" in p], ids=lambda p: os.path.basename(p)[5:-4])
+def test_module_bf16_autocast(cuda, path):
+    """LGM trains under bf16 mixed precision: the qkv Linear emits bf16 and the kernel runs in bf16."""
+    meta, z, params, grads = _load(path)
+    m = _module(meta).to(cuda)
+    m.load_state_dict(params, strict=True)
+    x = torch.from_numpy(z["x"]).to(cuda).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    y.float().backward(torch.from_numpy(z["gy"]).to(cuda))
+    assert rel_l2(y.detach().float().cpu().numpy(), z["y"]) < 3e-2
+    assert rel_l2(x.grad.float().cpu().numpy(), z["dx"]) < 5e-2
+
+
+SHAPES = [  # B, L, H, D -- LGM levels (4 views x 8^2 / 16^2 / 32^2 tokens, D = 64 / 64 / 32) and ragged edges
+    (1, 256, 16, 64), (2, 1024, 16, 64), (1, 4096, 16, 32), (1, 1, 2, 32), (3, 65, 2, 64), (2, 100, 3, 128),
+    (1, 17, 1, 32), (2, 600, 4, 32),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2), (torch.float16, 3e-3)],
+                         ids=["f32", "bf16", "f16"])
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_packed_attention_vs_fp64(cuda, shape, dtype, tol):
+    from lgm_amd.attention import packed_attention
+    B, L, H, D = shape
+    g = torch.Generator(device="cpu").manual_seed(B * 7919 + L * 31 + H * 7 + D)
+    qkv = (torch.randn((B, L, 3, H, D), generator=g) * 1.5).to(cuda, dtype)
+    d_o = torch.randn((B, L, H, D), generator=g).to(cuda, dtype)
+    scale = D ** -0.5
+    x = qkv.clone().requires_grad_(True)
+    o = packed_attention(x, scale)
+    o.backward(d_o)
+    o = o.detach()
+    torch.cuda.synchronize()
+    o_t, dqkv_t = _packed_truth(qkv, scale, d_o)
+    assert o.dtype == dtype and x.grad.dtype == dtype
+    assert torch.isfinite(o).all() and torch.isfinite(x.grad).all()
+    assert rel_l2(o.double().cpu().numpy(), o_t.cpu().numpy()) < tol
+    # per-slice relative L2, normalised by at least 1% of the whole dqkv norm: with L = 1 the softmax is constant
+    # and the true dq is exactly 0 (only rounding noise of dP - delta remains)
+    floor = 1e-2 * float(dqkv_t.norm())
+    for i, name in enumerate("qkv"):
+        a, b = x.grad[:, :, i].double(), dqkv_t[:, :, i]
+        err = float((a - b).norm()) / max(float(b.norm()), floor)
+        assert err < tol, (name, err)
+
+
+@pytest.mark.gpu
+def test_memory_efficient_attention_views_and_copies(cuda):
+    """xformers-style entry: unbind views of the packed tensor run in place; unrelated q/k/v are stacked."""
+    from lgm_amd.attention import memory_efficient_attention
+    B, L, H, D = 2, 130, 4, 32
+    qkv = torch.randn(B, L, 3, H, D, device=cuda)
+    q, k, v = torch.unbind(qkv, 2)
+    o1 = memory_efficient_attention(q, k, v)
+    o2 = memory_efficient_attention(q.contiguous(), k.contiguous(), v.contiguous())
+    assert torch.equal(o1, o2)
+    o_t, _ = _packed_truth(qkv, D ** -0.5, torch.zeros(B, L, H, D, device=cuda))
+    assert rel_l2(o1.double().cpu().numpy(), o_t.cpu().numpy()) < 1e-4
+
+
+@pytest.mark.gpu
+def test_attention_deterministic(cuda):
+    from lgm_amd.attention import packed_attention
+    qkv = torch.randn(1, 1024, 3, 16, 64, device=cuda, dtype=torch.bfloat16)
+    d_o = torch.randn(1, 1024, 16, 64, device=cuda, dtype=torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        x = qkv.clone().requires_grad_(True)
+        o = packed_attention(x)
+        o.backward(d_o)
+        outs.append((o, x.grad))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

@@ -69,23 +69,21 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
     import torch
-    import torch.distributed as dist
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    from lgm_amd import dist as D
+    info = D.rank_info()
+    rank, world = info.rank, info.world
+    torch.cuda.set_device(info.local)
+    dev = torch.device("cuda", info.local)
+    D.init("nccl", info, dev)
 
     from lgm_amd import GaussianRenderer, Options, _native
     from lgm_amd.cameras import orbit_cameras
     from lgm_amd.gs import count_pairs
     from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads
 
-    seed = 1 + rank
+    seed = D.scene_seed(rank)
     g_cpu = synthetic_gaussians(1, N_GAUSS, seed=seed)
     cv, cvp, cp = orbit_cameras(VIEWS)
     d_img, _, d_alpha, bg = synthetic_upstream_grads(1, VIEWS, RES, RES, seed=seed + 1000)
@@ -101,28 +99,13 @@ def main():
         torch.autograd.backward([out["image"], out["alpha"]], [d_imgd, d_alphad])
         g.grad = None
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
     for _ in range(args.warmup):
         step()
     prof = _native.KernelProfiler()
-    barrier()
-    torch.cuda.synchronize()
     with prof:
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        barrier()
-        el = time.perf_counter() - t0
+        el = D.timed_steps(step, args.steps, info, torch.cuda.synchronize, dev)
     kern = prof.summary()
     prof.close()
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el = float(el_t.item())
 
     P = RES * RES
     pixels = world * VIEWS * P * args.steps
@@ -163,8 +146,7 @@ def main():
                                               args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    D.finalize(info)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,97 @@
+"""Scene-sharded multi-GPU execution of the render path: one process per GPU, no data-path collective.
+
+The reference renders every object of a batch on its own (core/gs.py:42-93, a Python loop over B) and trains
+with accelerate's DDP: objects are split across ranks and only the UNet's parameter gradients are
+all-reduced, by DDP, outside this path. So the render path shards by object (scene): rank r owns objects
+shard_range(B, r, world); ranks never exchange splats, pixels or per-Gaussian gradients. The only collectives
+here are the barrier and the max-over-ranks time reduction of the bench (torch.distributed: RCCL on GPUs,
+gloo in the CPU tests).
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass
+from typing import Callable
+
+
+@dataclass(frozen=True)
+class RankInfo:
+    rank: int
+    world: int
+    local: int
+
+
+def rank_info() -> RankInfo:
+    """RANK / WORLD_SIZE / LOCAL_RANK as set by torch.distributed.run (defaults: a single process)."""
+    return RankInfo(int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+                    int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def init(backend: str, info: RankInfo, device=None) -> None:
+    """Initialise the default process group when world > 1 (env:// rendezvous; MASTER_ADDR 127.0.0.1 on one node)."""
+    if info.world <= 1:
+        return
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        kw = {"device_id": device} if (device is not None and backend == "nccl") else {}
+        dist.init_process_group(backend, rank=info.rank, world_size=info.world, **kw)
+
+
+def finalize(info: RankInfo) -> None:
+    if info.world > 1:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous, balanced split of n objects over world ranks (sizes differ by at most one)."""
+    base, extra = divmod(n, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def scene_seed(rank: int, base: int = 1) -> int:
+    """Seed of the synthetic scene rank `rank` renders in the weak-scaling bench (one distinct scene per GPU)."""
+    return base + rank
+
+
+def barrier(info: RankInfo) -> None:
+    if info.world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, info: RankInfo, device=None) -> float:
+    if info.world <= 1:
+        return float(x)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed_steps(step: Callable[[], None], steps: int, info: RankInfo, sync: Callable[[], None],
+                device=None) -> float:
+    """Time exactly `steps` calls of step(): barrier + sync on both sides, wall time maxed over ranks (seconds)."""
+    barrier(info)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier(info)
+    return max_over_ranks(time.perf_counter() - t0, info, device)
+
+
+def allreduce_scene_grads(grad, info: RankInfo):
+    """View-sharded variant: when the V views of ONE scene are split over ranks
+    (views shard_range(V, rank, world)), each rank's dL/dgaussians holds only its views' contributions; one
+    in-place SUM all-reduce (RCCL over xGMI: 2(G-1)/G x 56 N bytes per GPU) completes the per-scene sum that
+    the single-GPU backward does across views."""
+    if info.world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(grad, op=dist.ReduceOp.SUM)
+    return grad

@@ -1,0 +1,120 @@
+"""Multi-rank paths on CPU (gloo, world_size 2, 127.0.0.1): scene sharding with no data-path collective, the
+view-sharded variant with one gradient all-reduce, and the bench's barrier + max-over-ranks timing
+(lgm_amd/dist.py). The per-rank render is the CPU oracle (test infrastructure) standing in for the GPU kernels,
+which cannot run here; the GPU path shares every line of the sharding logic."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from lgm_amd import dist as D
+
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _scene(B, V, N, seed, H=32):
+    from lgm_amd.cameras import orbit_cameras
+    from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads
+    g = synthetic_gaussians(B, N, seed=seed)
+    cv, cvp, _ = orbit_cameras(V)
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(B, V, H, H, seed=seed + 7)
+    return g, cv[None].expand(B, V, 4, 4), cvp[None].expand(B, V, 4, 4), d_img, d_alpha, bg
+
+
+def _render(g, cv, cvp, d_img, d_alpha, bg, H=32):
+    from lgm_amd.cameras import tan_half_fov
+    from oracle import oracle as O
+    t = tan_half_fov(49.1)
+    return O.render(g.numpy(), cv.numpy(), cvp.numpy(), t, H, H, bg.numpy(), d_image=d_img.numpy(),
+                    d_alpha=d_alpha.numpy(), nthreads=1)
+
+
+def _worker(rank, port, tmp, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    info = D.rank_info()
+    D.init("gloo", info)
+    try:
+        if mode == "scenes":
+            B = 5  # ragged over 2 ranks: 3 + 2 objects
+            g, cv, cvp, d_img, d_alpha, bg = _scene(B, 2, 300, seed=11)
+            s0, s1 = D.shard_range(B, info.rank, info.world)
+            out = _render(g[s0:s1], cv[s0:s1], cvp[s0:s1], d_img[s0:s1], d_alpha[s0:s1], bg)
+            np.savez(os.path.join(tmp, f"r{rank}.npz"), image=out["image"], dg=out["d_gaussians"],
+                     rng=np.array([s0, s1]))
+        elif mode == "views":
+            V = 5
+            g, cv, cvp, d_img, d_alpha, bg = _scene(1, V, 300, seed=12)
+            v0, v1 = D.shard_range(V, info.rank, info.world)
+            out = _render(g, cv[:, v0:v1], cvp[:, v0:v1], d_img[:, v0:v1], d_alpha[:, v0:v1], bg)
+            dg = torch.from_numpy(out["d_gaussians"].astype(np.float64))
+            D.allreduce_scene_grads(dg, info)
+            np.savez(os.path.join(tmp, f"r{rank}.npz"), dg=dg.numpy())
+        elif mode == "timing":
+            import time
+            calls = []
+            dt = 0.05 * (1 + rank)  # rank 1 is the slow one
+
+            def step():
+                calls.append(1)
+                time.sleep(dt)
+
+            el = D.timed_steps(step, 3, info, sync=lambda: None)
+            np.savez(os.path.join(tmp, f"r{rank}.npz"), el=np.array(el), calls=np.array(len(calls)))
+    finally:
+        D.finalize(info)
+
+
+def _run(mode, tmp):
+    mp.start_processes(_worker, args=(_free_port(), str(tmp), mode), nprocs=WORLD, start_method="spawn")
+    return [np.load(os.path.join(tmp, f"r{r}.npz")) for r in range(WORLD)]
+
+
+def test_shard_range():
+    for n in range(0, 20):
+        for w in range(1, 9):
+            rs = [D.shard_range(n, r, w) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            sizes = [b - a for a, b in rs]
+            assert max(sizes) - min(sizes) <= 1
+    assert D.scene_seed(0) != D.scene_seed(1)
+
+
+def test_scene_sharded_equals_single_process(tmp_path):
+    res = _run("scenes", tmp_path)
+    g, cv, cvp, d_img, d_alpha, bg = _scene(5, 2, 300, seed=11)
+    full = _render(g, cv, cvp, d_img, d_alpha, bg)
+    for r in res:
+        s0, s1 = r["rng"]
+        np.testing.assert_array_equal(r["image"], full["image"][s0:s1])
+        np.testing.assert_array_equal(r["dg"], full["d_gaussians"][s0:s1])
+    assert sum(int(r["rng"][1] - r["rng"][0]) for r in res) == 5
+
+
+def test_view_sharded_allreduce(tmp_path):
+    res = _run("views", tmp_path)
+    g, cv, cvp, d_img, d_alpha, bg = _scene(1, 5, 300, seed=12)
+    full = _render(g, cv, cvp, d_img, d_alpha, bg)["d_gaussians"]
+    for r in res:
+        np.testing.assert_allclose(r["dg"], full, rtol=1e-5, atol=1e-7 * np.abs(full).max())
+    np.testing.assert_array_equal(res[0]["dg"], res[1]["dg"])
+
+
+def test_timed_steps_max_over_ranks(tmp_path):
+    res = _run("timing", tmp_path)
+    els = [float(r["el"]) for r in res]
+    assert els[0] == els[1]  # every rank reports the max
+    assert els[0] >= 3 * 0.1 * 0.95  # the slow rank's 3 x 0.1 s
+    assert all(int(r["calls"]) == 3 for r in res)

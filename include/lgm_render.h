@@ -57,7 +57,7 @@ int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians
                        const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                        float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
                        void *workspace, size_t workspace_bytes, long long pair_capacity, long long *stats_out,
-                       void *stream);
+                       int options, void *stream);
 
 /* Backward of all B x V renders (replaces B*V calls of _C.rasterize_gaussians_backward plus the autograd sum
  * over views). d_depth / d_alpha may be NULL (treated as zero). Writes d_gaussians [B,N,14] (overwrites).
@@ -66,16 +66,25 @@ int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussian
                         const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
                         float *d_gaussians, float *d_means2D, void *workspace, size_t workspace_bytes,
-                        long long pair_capacity, void *stream);
+                        long long pair_capacity, int options, void *stream);
 
 /* Diagnostics: while device_counters (a DEVICE uint64[8], caller-zeroed) is set, the render kernels add work
  * counts to it: [0] forward wavefront-entry iterations, [1] accepted (pixel, Gaussian) contributions,
  * [2] backward wavefront-entry iterations, [3] backward (pixel, Gaussian) gradient contributions,
  * [4] dense / [5] sparse wavefront reductions, [6] tile-list entries staged by the forward, [7] max forward
- * iterations of one wavefront; then per tile workgroup (B*V*T of them) 4 s_memrealtime stamps (100 MHz):
- * [8+4t] fwd start, [8+4t+1] fwd end, [8+4t+2] bwd start (after the early exit test), [8+4t+3] bwd end -- so
- * the buffer must hold 8 + 4*B*V*tiles entries. NULL disables (default). Process-wide; not for concurrent use. */
+ * iterations of one wavefront; then 8 entries per tile t (B*V*T tiles): s_memrealtime stamps (100 MHz)
+ * [8+8t] fwd start, [+1] fwd end, [+2] bwd start (after the early exit test), [+3] bwd end, [+4] sort start,
+ * [+5] sort end, and [+6] the tile's binned list length; then 8 entries per binning workgroup
+ * (B*V*ceil(N/1024)): phase stamps [0] start, [1] preprocessed, [2] tile tests done, [3] reserved, [4] end,
+ * and [5] its binned pairs -- so the buffer must hold 8 + 8*B*V*tiles + 8*B*V*ceil(N/1024) entries.
+ * NULL disables (default). Process-wide; not for concurrent use. */
 int lgm_render_debug_counters(unsigned long long *device_counters);
+
+/* Per-call `options` of lgm_render_forward / lgm_render_backward (pass the same value to both).
+ * LGM_RENDER_CLAMP_IMAGE: the forward writes clamp(image, 0, 1) (core/gs.py:87) and keeps a per-pixel mask in
+ * the workspace; the backward passes d_image only where 0 <= unclamped <= 1 (torch's clamp gradient), so no
+ * separate clamp kernels or unclamped copy are needed. */
+#define LGM_RENDER_CLAMP_IMAGE 2
 
 /* Option flags (process-wide, default 0). LGM_RENDER_NO_CULL bins upstream's full 3-sigma tile rects instead of
  * dropping (Gaussian, tile) pairs where alpha < 1/255 is provable for every pixel; outputs are identical either

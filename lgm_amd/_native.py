@@ -23,9 +23,9 @@ SIGNATURES = {
     "lgm_render_count_pairs": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_float, _c_float,
                                         _c_float, _vp, _c_size, _vp, _vp]),
     "lgm_render_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_float,
-                                    _c_float, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _vp, _vp]),
+                                    _c_float, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _vp, _c_int, _vp]),
     "lgm_render_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_float,
-                                     _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _vp]),
+                                     _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _c_int, _vp]),
     "lgm_attn_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
                                   _vp]),
     "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
@@ -41,6 +41,10 @@ SIGNATURES = {
 }
 
 _lib = None
+
+
+ABI_VERSION = 2
+RENDER_CLAMP_IMAGE = 2  # include/lgm_render.h LGM_RENDER_CLAMP_IMAGE
 
 
 class NativeError(RuntimeError):
@@ -59,6 +63,8 @@ def lib():
                 continue
             fn.restype = res
             fn.argtypes = args
+        if L.lgm_abi_version() != ABI_VERSION:
+            raise NativeError(f"{LIB_PATH}: ABI {L.lgm_abi_version()} != {ABI_VERSION}; rebuild (python -m lgm_amd.build)")
         _lib = L
     return _lib
 

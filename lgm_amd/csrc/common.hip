@@ -64,7 +64,7 @@ void prof_end(hipStream_t st) {
 
 extern "C" {
 const char *lgm_last_error(void) { return lgm::g_err; }
-int lgm_abi_version(void) { return 1; }
+int lgm_abi_version(void) { return 2; }
 
 lgm_profiler *lgm_profiler_create(void) { return new lgm_profiler(); }
 int lgm_profiler_attach(lgm_profiler *p) {

@@ -37,6 +37,7 @@ int check_common(int B, int V, int N, int H, int W, const void *g, const void *c
     d.mod = mod;
     d.counters = g_counters;
     d.flags = g_flags;
+    d.options = 0;
     return LGM_OK;
 }
 
@@ -85,7 +86,7 @@ int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians
                        const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                        float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
                        void *workspace, size_t workspace_bytes, long long pair_capacity, long long *stats_out,
-                       void *stream) {
+                       int options, void *stream) {
     lgm::clear_error();
     lgm::Dims d;
     int rc = check_common(B, V, N, H, W, gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, scale_modifier, d);
@@ -103,6 +104,7 @@ int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians
         lgm::set_error("workspace too small (%zu < %zu)", workspace_bytes, L.total);
         return LGM_E_WORKSPACE;
     }
+    d.options = options;
     char *ws = (char *)workspace;
     hipStream_t st = (hipStream_t)stream;
     rc = lgm::launch_binning(d, gaussians, cam_view, cam_view_proj, ws, L, radii_out, stats_out, false, st);
@@ -114,7 +116,7 @@ int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussian
                         const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
                         float *d_gaussians, float *d_means2D, void *workspace, size_t workspace_bytes,
-                        long long pair_capacity, void *stream) {
+                        long long pair_capacity, int options, void *stream) {
     lgm::clear_error();
     lgm::Dims d;
     int rc = check_common(B, V, N, H, W, gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, scale_modifier, d);
@@ -129,6 +131,7 @@ int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussian
         return LGM_E_WORKSPACE;
     }
     if (N == 0) return LGM_OK;
+    d.options = options;
     return lgm::launch_render_bwd(d, gaussians, cam_view, cam_view_proj, bg, d_image, d_depth, d_alpha, d_gaussians,
                                   d_means2D, (char *)workspace, L, (hipStream_t)stream);
 }

@@ -19,132 +19,225 @@ namespace {
 
 enum BinMode { COUNT = 0, EMIT_SLOT = 1, EMIT_PACKED = 2 };
 
-// ------------------------------------------------------------------------------------------------------------
-// k_bin: grid (ceil(N / BIN_G), B*V), block 256; every thread handles BIN_GPT Gaussians of one view so that a
-// workgroup's LDS tile histogram aggregates 1024 Gaussians before its one global reservation per touched tile.
-constexpr int BIN_GPT = 4, BIN_G = 256 * BIN_GPT;
+__device__ __forceinline__ int wave_incl_scan(int x, int lane) {
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+        const int y = __shfl_up(x, dd, 64);
+        if (lane >= dd) x += y;
+    }
+    return x;
+}
 
-struct EmitGeo {
+// ------------------------------------------------------------------------------------------------------------
+// k_bin: grid (ceil(N / BIN_G), B*V), block BIN_THREADS, one Gaussian per thread. A workgroup's LDS tile
+// histogram aggregates its BIN_G Gaussians before one global reservation per touched tile.
+//
+// Load balance: a Gaussian's work is its candidate-tile rectangle (1 to hundreds of tiles). Each wavefront
+// flattens the candidates of its 64 Gaussians into one list and tests 64 at a time (lane -> candidate; the owner
+// Gaussian found by a head-flag max-scan), so no lane idles behind a large Gaussian. Hits are recorded in an LDS
+// hit list with their rank in the tile (returned by the histogram atomic), and the emission after the global
+// reservation is a flat loop over that list.
+#ifndef LGM_BIN_THREADS
+#define LGM_BIN_THREADS 512
+#endif
+constexpr int BIN_THREADS = LGM_BIN_THREADS, BIN_G = BIN_THREADS;
+constexpr int BIN_HITCAP = BIN_THREADS * 6;  // hit-list capacity (typical: ~4 hits per Gaussian)
+static_assert(BIN_THREADS <= 512, "owner index packs into 9 bits");
+
+struct BinRec {  // one Gaussian's emit record in LDS (48 B)
     float x, y, A, B, C, iA, iC, tau;
-    int cx0, cy0, cx1, cy1;
-    unsigned long long hitmask;  // candidate tiles (row-major in the candidate rect) that pass the exact test
+    unsigned c0;  // cx0 | cy0 << 16
+    unsigned w;   // candidate rect width
     unsigned long long key;
 };
 
+__device__ __forceinline__ int wave_incl_max(int v, int lane) {
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+        const int y = __shfl_up(v, dd, 64);
+        if (lane >= dd) v = max(v, y);
+    }
+    return v;
+}
+
 template <int MODE>
-__global__ __launch_bounds__(256) void k_bin(Dims d, const float *__restrict__ gauss, const float *__restrict__ views,
-                                             const float *__restrict__ projs, float4 *__restrict__ gA,
-                                             float4 *__restrict__ gB, float *__restrict__ gD,
-                                             uint2 *__restrict__ rects, int *__restrict__ radii_out,
-                                             int *__restrict__ tile_count, const int *__restrict__ tile_start,
-                                             unsigned long long *__restrict__ pairs, long long slot_stride,
-                                             unsigned long long *__restrict__ misc) {
-    extern __shared__ int hist[];  // [T] counts, then [T] reserved bases
+__global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__restrict__ gauss, const float *__restrict__ views,
+                                                     const float *__restrict__ projs, float4 *__restrict__ gA,
+                                                     float4 *__restrict__ gB, float *__restrict__ gD,
+                                                     uint2 *__restrict__ rects, int *__restrict__ radii_out,
+                                                     int *__restrict__ tile_count, const int *__restrict__ tile_start,
+                                                     unsigned long long *__restrict__ pairs, long long slot_stride,
+                                                     unsigned long long *__restrict__ misc, float *__restrict__ accum) {
+    extern __shared__ int hist[];  // [T] per-tile hit counts, [T] reserved global bases, [T] fallback cursors
+    __shared__ BinRec srec[BIN_THREADS];
+    __shared__ int sHead[BIN_THREADS], sExcl[BIN_THREADS];
+    __shared__ unsigned sHit[BIN_HITCAP];         // owner | tile << 9
+    __shared__ unsigned short sRank[BIN_HITCAP];  // rank of the hit within its tile (this workgroup)
+    __shared__ int s_nhit;
     __shared__ unsigned long long s_tot[2];
-    const int bv = blockIdx.y, b = bv / d.V, T = d.T;
+    const int bv = blockIdx.y, b = bv / d.V, T = d.T, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const bool lds = T <= LDS_HIST_MAX;
-    int *hbase = hist + T;
+    int *hbase = hist + T, *fill = hist + 2 * T;
     int *cur = tile_count + (size_t)bv * T;
-    if (threadIdx.x < 2) s_tot[threadIdx.x] = 0;
+    if (tid < 2) s_tot[tid] = 0;
+    if (tid == 0) s_nhit = 0;
     if (lds)
-        for (int t = threadIdx.x; t < T; t += blockDim.x) hist[t] = 0;
-    __syncthreads();
+        for (int t = tid; t < T; t += BIN_THREADS) hist[t] = 0;
     auto dest = [&](int t, int pos) -> long long {
         return (MODE == EMIT_SLOT ? ((long long)bv * T + t) * slot_stride
                                   : (long long)tile_start[(size_t)bv * T + t]) + pos;
     };
-    EmitGeo em[BIN_GPT];
-    unsigned long long nemit = 0, nref = 0;
+    // diagnostics: per-workgroup phase stamps after the per-tile records (see lgm_render_debug_counters)
+    unsigned long long *stamp = d.counters ? d.counters + 8 + 8 * (size_t)d.BV * T +
+                                             8 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x)
+                                           : nullptr;
+    if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
+    // ---- preprocess, one Gaussian per thread
+    const int i = blockIdx.x * BIN_G + tid;
+    Geo o;
+    bool vis = false;
+    if (i < d.N) {
+        float g[14];
+        load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
+        vis = preprocess_one(g, views + 16 * bv, projs + 16 * bv, d, o);
+        if (MODE != COUNT) {
+            const size_t k = (size_t)bv * d.N + i;
+            if (vis) {
+                gA[k] = make_float4(o.x, o.y, o.tau, 0.f);
+                gB[k] = make_float4(o.A, o.B, o.C, o.opacity);
+                gD[k] = o.depth;
+                rects[k] = make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16), (unsigned)o.x1 | ((unsigned)o.y1 << 16));
+                // the backward's per-view gradient accumulators start at zero (k_preproc_bwd re-zeroes them)
+                float2 *a2 = reinterpret_cast<float2 *>(accum + k * NACC);
 #pragma unroll
-    for (int r = 0; r < BIN_GPT; r++) {
-        const int i = blockIdx.x * BIN_G + r * 256 + threadIdx.x;
-        Geo o;
-        bool vis = false;
-        if (i < d.N) {
-            float g[14];
-            load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
-            vis = preprocess_one(g, views + 16 * bv, projs + 16 * bv, d, o);
-            if (MODE != COUNT) {
-                const size_t k = (size_t)bv * d.N + i;
-                if (vis) {
-                    gA[k] = make_float4(o.x, o.y, o.tau, 0.f);
-                    gB[k] = make_float4(o.A, o.B, o.C, o.opacity);
-                    gD[k] = o.depth;
-                    rects[k] = make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16),
-                                          (unsigned)o.x1 | ((unsigned)o.y1 << 16));
-                } else {
-                    gA[k] = make_float4(0.f, 0.f, -1.f, 0.f);
-                    gB[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    gD[k] = 0.f;
-                    rects[k] = make_uint2(0u, 0u);
-                }
-                if (radii_out) radii_out[k] = vis ? o.radius : 0;
+                for (int q = 0; q < NACC / 2; q++) a2[q] = make_float2(0.f, 0.f);
+            } else {
+                gA[k] = make_float4(0.f, 0.f, -1.f, 0.f);
+                gB[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                gD[k] = 0.f;
+                rects[k] = make_uint2(0u, 0u);
             }
+            if (radii_out) radii_out[k] = vis ? o.radius : 0;
         }
-        EmitGeo &e = em[r];
-        e.hitmask = 0ull;
-        if (!vis) {
-            e.cx0 = e.cx1 = e.cy0 = e.cy1 = 0;
-            e.key = 0ull;
-            continue;
-        }
-        nref += (unsigned long long)((o.x1 - o.x0) * (o.y1 - o.y0));
-        e.x = o.x; e.y = o.y; e.A = o.A; e.B = o.B; e.C = o.C; e.tau = o.tau;
-        e.iA = 1.0f / o.A;
-        e.iC = 1.0f / o.C;
-        e.cx0 = o.cx0; e.cy0 = o.cy0; e.cx1 = o.cx1; e.cy1 = o.cy1;
-        e.key = ((unsigned long long)__float_as_uint(o.depth) << 32) | (unsigned)i;
-        int bit = 0;
-        for (int y = e.cy0; y < e.cy1; y++)
-            for (int x = e.cx0; x < e.cx1; x++, bit++) {
-                if (!ellipse_hits_rect(e.x, e.y, e.A, e.B, e.C, e.iA, e.iC, e.tau, (float)(x * BX),
-                                       (float)(x * BX + BX - 1), (float)(y * BY), (float)(y * BY + BY - 1)))
-                    continue;
-                nemit++;
-                if (bit < 64) e.hitmask |= 1ull << bit;
-                const int t = y * d.gx + x;
-                if (lds) {
-                    atomicAdd(&hist[t], 1);
-                } else {
-                    const int pos = atomicAdd(&cur[t], 1);
-                    if (MODE != COUNT) pairs[dest(t, pos)] = e.key;
-                }
-            }
     }
-    if (nemit) atomicAdd(&s_tot[0], nemit);
-    if (nref) atomicAdd(&s_tot[1], nref);
+    int nc = 0;
+    unsigned long long nref = 0;
+    if (vis) {
+        BinRec r;
+        r.x = o.x; r.y = o.y; r.A = o.A; r.B = o.B; r.C = o.C; r.tau = o.tau;
+        r.iA = 1.0f / o.A;
+        r.iC = 1.0f / o.C;
+        r.c0 = (unsigned)o.cx0 | ((unsigned)o.cy0 << 16);
+        r.w = (unsigned)(o.cx1 - o.cx0);
+        r.key = ((unsigned long long)__float_as_uint(o.depth) << 32) | (unsigned)i;
+        srec[tid] = r;
+        nc = (o.cx1 - o.cx0) * (o.cy1 - o.cy0);
+        nref = (unsigned long long)((o.x1 - o.x0) * (o.y1 - o.y0));
+    }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) nref += __shfl_xor(nref, o2, 64);
+    if (lane == 0 && nref) atomicAdd(&s_tot[1], nref);
+    // ---- flattened exact tile tests of the wavefront's candidates
+    const int incl = wave_incl_scan(nc, lane), excl = incl - nc;
+    const int total = __shfl(incl, 63, 64);
+    sExcl[tid] = excl;
+    __syncthreads();  // histogram zeroed; records and exclusive offsets visible
+    if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned long long nemit = 0;  // wave-uniform
+    int carry = 0;
+    for (int base0 = 0; base0 < total; base0 += 64) {
+        sHead[tid] = -1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (nc > 0 && excl >= base0 && excl < base0 + 64) sHead[w * 64 + excl - base0] = lane;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        int v = sHead[tid];
+        if (lane == 0 && v < 0) v = carry;
+        v = wave_incl_max(v, lane);
+        carry = __shfl(v, 63, 64);
+        const int c = base0 + lane;
+        bool hit = false;
+        int t = 0, owner = 0;
+        if (c < total) {
+            owner = w * 64 + v;
+            const BinRec &e = srec[owner];
+            const int j = c - sExcl[owner];
+            const int cw = (int)e.w;
+            int jy = (int)((float)j * __builtin_amdgcn_rcpf((float)cw));
+            int jx = j - jy * cw;
+            if (jx < 0) { jy--; jx += cw; }
+            if (jx >= cw) { jy++; jx -= cw; }
+            const int x = (int)(e.c0 & 0xffffu) + jx, y = (int)(e.c0 >> 16) + jy;
+            hit = ellipse_hits_rect(e.x, e.y, e.A, e.B, e.C, e.iA, e.iC, e.tau, (float)(x * BX),
+                                    (float)(x * BX + BX - 1), (float)(y * BY), (float)(y * BY + BY - 1));
+            t = y * d.gx + x;
+        }
+        const unsigned long long hm = __ballot(hit);
+        nemit += __popcll(hm);
+        if (!hm) continue;
+        if (lds) {
+            int slot0 = 0;
+            if (MODE != COUNT && lane == 0) slot0 = atomicAdd(&s_nhit, __popcll(hm));
+            slot0 = __shfl(slot0, 0, 64);
+            if (hit) {
+                const int rk = atomicAdd(&hist[t], 1);
+                if (MODE != COUNT) {
+                    const int slot = slot0 + __popcll(hm & lt);
+                    if (slot < BIN_HITCAP) {
+                        sHit[slot] = (unsigned)owner | ((unsigned)t << 9);
+                        sRank[slot] = (unsigned short)rk;
+                    }
+                }
+            }
+        } else if (hit) {
+            const int pos = atomicAdd(&cur[t], 1);
+            if (MODE != COUNT) pairs[dest(t, pos)] = srec[owner].key;
+        }
+    }
+    if (lane == 0 && nemit) atomicAdd(&s_tot[0], nemit);
     if (lds) {
         __syncthreads();
-        for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
+        for (int t = tid; t < T; t += BIN_THREADS) {
             const int c = hist[t];
-            if (MODE == COUNT) {
-                if (c) atomicAdd(&cur[t], c);
-            } else {
-                if (c) hbase[t] = atomicAdd(&cur[t], c);
-                hist[t] = 0;
+            if (c) {
+                if (MODE == COUNT) atomicAdd(&cur[t], c);
+                else hbase[t] = atomicAdd(&cur[t], c);
             }
+            fill[t] = 0;
         }
+        __syncthreads();
+        if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
         if (MODE != COUNT) {
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < BIN_GPT; r++) {
-                const EmitGeo &e = em[r];
-                int bit = 0;
-                for (int y = e.cy0; y < e.cy1; y++)
-                    for (int x = e.cx0; x < e.cx1; x++, bit++) {
-                        const bool h = bit < 64 ? ((e.hitmask >> bit) & 1ull) != 0ull
-                                                : ellipse_hits_rect(e.x, e.y, e.A, e.B, e.C, e.iA, e.iC, e.tau,
-                                                                    (float)(x * BX), (float)(x * BX + BX - 1),
-                                                                    (float)(y * BY), (float)(y * BY + BY - 1));
-                        if (!h) continue;
+            const int H = s_nhit;
+            if (H <= BIN_HITCAP) {
+                for (int h = tid; h < H; h += BIN_THREADS) {
+                    const unsigned e2 = sHit[h];
+                    const int t = (int)(e2 >> 9);
+                    pairs[dest(t, hbase[t] + sRank[h])] = srec[e2 & 511u].key;
+                }
+            } else {
+                // hit list overflow (unusually dense workgroup): re-test this thread's own Gaussian's candidates
+                const BinRec &e = srec[tid];
+                const int cw = vis ? (int)e.w : 0, chh = cw ? nc / cw : 0;
+                const int cx0 = (int)(e.c0 & 0xffffu), cy0 = (int)(e.c0 >> 16);
+                for (int y = cy0; y < cy0 + chh; y++)
+                    for (int x = cx0; x < cx0 + cw; x++) {
+                        if (!ellipse_hits_rect(e.x, e.y, e.A, e.B, e.C, e.iA, e.iC, e.tau, (float)(x * BX),
+                                               (float)(x * BX + BX - 1), (float)(y * BY), (float)(y * BY + BY - 1)))
+                            continue;
                         const int t = y * d.gx + x;
-                        pairs[dest(t, hbase[t] + atomicAdd(&hist[t], 1))] = e.key;
+                        pairs[dest(t, hbase[t] + atomicAdd(&fill[t], 1))] = e.key;
                     }
             }
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (stamp && tid == 0) {
+        stamp[4] = __builtin_amdgcn_s_memrealtime();
+        stamp[5] = (unsigned long long)s_nhit;
+    }
+    if (tid == 0) {
         atomicAdd(&misc[0], s_tot[0]);
         atomicAdd(&misc[1], s_tot[1]);
     }
@@ -185,16 +278,27 @@ __global__ __launch_bounds__(1024) void k_scan(const int *__restrict__ count, in
 }
 
 // ------------------------------------------------------------------------------------------------------------
-constexpr int RS_THREADS = 512, RS_WAVES = RS_THREADS / 64, RS_CAP = 8192, RS_MAXR = RS_CAP / RS_THREADS;
-constexpr int RS_LDS = RS_CAP * 8 + RS_WAVES * 256 * 4;
+// Per-tile sort: RS_CAP entries sorted in LDS (larger buckets take sort_oversized): u32 keys, u16 bucket positions
+// and per-wave 512-bucket counters (40 KB at 512 threads; 8 rows per lane keep it at ~90 VGPRs).
+#ifndef LGM_RS_THREADS
+#define LGM_RS_THREADS 512
+#endif
+#ifndef LGM_RS_CAP
+#define LGM_RS_CAP 4096
+#endif
+constexpr int RS_THREADS = LGM_RS_THREADS, RS_WAVES = RS_THREADS / 64, RS_CAP = LGM_RS_CAP,
+              RS_MAXR = RS_CAP / RS_THREADS;
+constexpr int RS_DBITS = 9, RS_B = 1 << RS_DBITS;  // digit width: a typical 26-bit depth span takes 3 passes
+constexpr int RS_LDS = RS_CAP * 4 + RS_CAP * 2 + RS_WAVES * RS_B * 4;
+static_assert(RS_LDS >= RS_CAP * 8, "sort_oversized reuses the image as u64[RS_CAP]");
+static_assert(RS_B % RS_THREADS == 0 || RS_THREADS % RS_B == 0, "bucket scan layout");
 
 __device__ __forceinline__ unsigned long long lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
 
-// Lanes of the wavefront holding the same 8-bit digit as this lane (restricted to valid lanes).
-__device__ __forceinline__ unsigned long long match8(unsigned dgt, bool valid) {
+// Lanes of the wavefront holding the same nbits-bit digit as this lane (restricted to valid lanes).
+__device__ __forceinline__ unsigned long long match_digit(unsigned dgt, bool valid, int nbits) {
     unsigned long long peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; b++) {
+    for (int b = 0; b < nbits; b++) {
         const bool bit = (dgt >> b) & 1u;
         const unsigned long long m = __ballot(bit);
         peers &= bit ? m : ~m;
@@ -212,62 +316,67 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o, 64));
     return v;
 }
-__device__ __forceinline__ int wave_incl_scan(int x, int lane) {
-#pragma unroll
-    for (int dd = 1; dd < 64; dd <<= 1) {
-        const int y = __shfl_up(x, dd, 64);
-        if (lane >= dd) x += y;
-    }
-    return x;
-}
 
-// One stable LSD pass over 8-bit digits (kr >> shift) & 255 of the per-wave chunks held in registers; writes
-// the permuted (key, value) pairs to LDS sk/sv. All threads of the block must call it.
-__device__ __forceinline__ void radix_pass(unsigned (&kr)[RS_MAXR], unsigned (&vr)[RS_MAXR], bool by_value,
-                                          int shift, int n, int c0, int R, unsigned *sk, unsigned *sv, int *cnt,
-                                          int *s_wsum) {
+// One stable LSD pass over the nbits-bit digit (kr >> shift) of the per-wave chunks held in registers, writing the permuted keys / bucket positions to sk / sp. Ranks come from ballot
+// matching (one leader per digit updates the wave's counter: no contended LDS atomics) and are kept in registers
+// for the scatter. All threads of the block call it.
+__device__ __forceinline__ void radix_pass(const unsigned (&kr)[RS_MAXR], const unsigned short (&pr)[RS_MAXR],
+                                          int shift, int nbits, int n, int c0, int R, unsigned *sk,
+                                          unsigned short *sp, int *cnt, int *s_wsum) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    int *my = cnt + w * 256;
-    for (int q = lane; q < 256; q += 64) my[q] = 0;
-#pragma unroll
-    for (int r = 0; r < RS_MAXR; r++) {
-        if (r < R) {
-            const int e = c0 + r * 64 + lane;
-            if (e < n) atomicAdd(&my[((by_value ? vr[r] : kr[r]) >> shift) & 255u], 1);
-        }
-    }
-    __syncthreads();
-    int run = 0, incl = 0;
-    if (tid < 256) {
-        for (int ww = 0; ww < RS_WAVES; ww++) {
-            const int x = cnt[ww * 256 + tid];
-            cnt[ww * 256 + tid] = run;
-            run += x;
-        }
-        incl = wave_incl_scan(run, lane);
-        if (lane == 63) s_wsum[w] = incl;
-    }
-    __syncthreads();
-    if (tid < 256) {
-        int off = incl - run;
-        for (int ww = 0; ww < w; ww++) off += s_wsum[ww];
-        for (int ww = 0; ww < RS_WAVES; ww++) cnt[ww * 256 + tid] += off;
-    }
-    __syncthreads();
+    const unsigned mask = (1u << nbits) - 1u;
+    int *my = cnt + w * RS_B;
+    for (int q = lane; q < RS_B; q += 64) my[q] = 0;
     const unsigned long long lt = lanemask_lt(lane);
+    int lr[RS_MAXR];
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
+        lr[r] = 0;
         if (r < R) {
             const int e = c0 + r * 64 + lane;
             const bool valid = e < n;
-            const unsigned dgt = ((by_value ? vr[r] : kr[r]) >> shift) & 255u;
-            const unsigned long long peers = match8(dgt, valid);
+            const unsigned dgt = (kr[r] >> shift) & mask;
+            const unsigned long long peers = match_digit(dgt, valid, nbits);
             if (valid) {
-                const int rank = __popcll(peers & lt);
-                const int pos = my[dgt] + rank;
-                if (rank == 0) my[dgt] += __popcll(peers);
+                const int rk = __popcll(peers & lt);
+                const int b0 = my[dgt];  // same address for all peers: broadcast read
+                lr[r] = b0 + rk;
+                if (rk == 0) my[dgt] = b0 + __popcll(peers);
+            }
+        }
+    }
+    __syncthreads();
+    // exclusive bases, bucket-major then wave: base(w, d) = sum_{d' < d} total(d') + sum_{w' < w} cnt[w'][d]
+    constexpr int BPT = RS_B / RS_THREADS > 0 ? RS_B / RS_THREADS : 1;  // buckets per thread (contiguous)
+    int tot = 0;
+    if (tid * BPT < RS_B) {
+#pragma unroll
+        for (int j = 0; j < BPT; j++)
+            for (int ww = 0; ww < RS_WAVES; ww++) tot += cnt[ww * RS_B + tid * BPT + j];
+    }
+    const int incl = wave_incl_scan(tot, lane);
+    if (lane == 63) s_wsum[w] = incl;
+    __syncthreads();
+    if (tid * BPT < RS_B) {
+        int run = incl - tot;
+        for (int ww = 0; ww < w; ww++) run += s_wsum[ww];
+#pragma unroll
+        for (int j = 0; j < BPT; j++)
+            for (int ww = 0; ww < RS_WAVES; ww++) {
+                const int x = cnt[ww * RS_B + tid * BPT + j];
+                cnt[ww * RS_B + tid * BPT + j] = run;
+                run += x;
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_MAXR; r++) {
+        if (r < R) {
+            const int e = c0 + r * 64 + lane;
+            if (e < n) {
+                const int pos = my[(kr[r] >> shift) & mask] + lr[r];
                 sk[pos] = kr[r];
-                sv[pos] = vr[r];
+                sp[pos] = pr[r];
             }
         }
     }
@@ -347,19 +456,14 @@ __device__ void sort_oversized(unsigned long long *seg, int n, unsigned long lon
     }
 }
 
-// k_sort: grid (B*V*T), block RS_THREADS, dynamic LDS RS_LDS bytes.
-__global__ __launch_bounds__(RS_THREADS) void k_sort(long long slot_stride, const int *__restrict__ tile_start,
-                                                     const int *__restrict__ tile_count,
-                                                     unsigned long long *__restrict__ pairs) {
+// One tile's bucket: LDS LSD radix sort (see the file header); all threads of the block call it.
+__device__ __forceinline__ void sort_tile(long long base, int n, unsigned long long *__restrict__ pairs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned *sk = reinterpret_cast<unsigned *>(smem);
-    unsigned *sv = sk + RS_CAP;
-    int *cnt = reinterpret_cast<int *>(sv + RS_CAP);
-    __shared__ unsigned s_min, s_max;
-    __shared__ int s_wsum[4], s_long;
-    long long base;
-    int n;
-    tile_range(blockIdx.x, slot_stride, tile_start, tile_count, base, n);
+    unsigned short *sp = reinterpret_cast<unsigned short *>(sk + RS_CAP);
+    int *cnt = reinterpret_cast<int *>(sp + RS_CAP);
+    __shared__ unsigned s_min, s_max, s_vmax;
+    __shared__ int s_wsum[RS_WAVES], s_long;
     if (n <= 1) return;  // a single id already sits in place (low half of its key)
     unsigned long long *seg = pairs + base;
     if (n > RS_CAP) {
@@ -369,50 +473,53 @@ __global__ __launch_bounds__(RS_THREADS) void k_sort(long long slot_stride, cons
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int C = ((n + RS_THREADS - 1) / RS_THREADS) * 64;  // per-wave chunk, a multiple of 64
     const int R = C >> 6, c0 = w * C;
-    unsigned kr[RS_MAXR], vr[RS_MAXR];
+    unsigned kr[RS_MAXR];
+    unsigned short pr[RS_MAXR];
     unsigned lmin = 0xffffffffu, lmax = 0u, vmax = 0u;
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         kr[r] = 0u;
-        vr[r] = 0u;
+        pr[r] = 0;
         const int e = c0 + r * 64 + lane;
         if (r < R && e < n) {
             const unsigned long long x = seg[e];
             kr[r] = (unsigned)(x >> 32);
-            vr[r] = (unsigned)x;
+            pr[r] = (unsigned short)e;
             lmin = min(lmin, kr[r]);
             lmax = max(lmax, kr[r]);
-            vmax = max(vmax, vr[r]);
+            vmax = max(vmax, (unsigned)x);
         }
     }
-    if (tid == 0) { s_min = 0xffffffffu; s_max = 0u; s_long = 0; }
+    if (tid == 0) { s_min = 0xffffffffu; s_max = 0u; s_vmax = 0u; s_long = 0; }
     __syncthreads();
     lmin = wave_min_u32(lmin);
     lmax = wave_max_u32(lmax);
-    if (lane == 0) { atomicMin(&s_min, lmin); atomicMax(&s_max, lmax); }
+    vmax = wave_max_u32(vmax);
+    if (lane == 0) { atomicMin(&s_min, lmin); atomicMax(&s_max, lmax); atomicMax(&s_vmax, vmax); }
     __syncthreads();
     const unsigned kmin = s_min, span = s_max - s_min;
-    const int kpasses = span ? (32 - __clz(span) + 7) >> 3 : 0;
+    const int kbits = span ? 32 - __clz(span) : 0;
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) kr[r] -= kmin;
-    for (int p = 0; p < kpasses; p++) {
-        radix_pass(kr, vr, false, 8 * p, n, c0, R, sk, sv, cnt, s_wsum);
-        if (p + 1 < kpasses) {
-#pragma unroll
-            for (int r = 0; r < RS_MAXR; r++) {
-                if (r < R) {
-                    const int e = c0 + r * 64 + lane;
-                    if (e < n) { kr[r] = sk[e]; vr[r] = sv[e]; }
-                }
-            }
-        }
-    }
-    if (kpasses == 0) {
+    auto reload = [&]() {
 #pragma unroll
         for (int r = 0; r < RS_MAXR; r++) {
             if (r < R) {
                 const int e = c0 + r * 64 + lane;
-                if (e < n) { sk[e] = kr[r]; sv[e] = vr[r]; }
+                if (e < n) { kr[r] = sk[e]; pr[r] = sp[e]; }
+            }
+        }
+    };
+    for (int sh = 0; sh < kbits; sh += RS_DBITS) {
+        radix_pass(kr, pr, sh, min(RS_DBITS, kbits - sh), n, c0, R, sk, sp, cnt, s_wsum);
+        reload();
+    }
+    if (kbits == 0) {
+#pragma unroll
+        for (int r = 0; r < RS_MAXR; r++) {
+            if (r < R) {
+                const int e = c0 + r * 64 + lane;
+                if (e < n) { sk[e] = kr[r]; sp[e] = pr[r]; }
             }
         }
         __syncthreads();
@@ -421,57 +528,100 @@ __global__ __launch_bounds__(RS_THREADS) void k_sort(long long slot_stride, cons
     for (int q = tid + 32; q < n; q += RS_THREADS)
         if (sk[q] == sk[q - 32]) s_long = 1;
     __syncthreads();
+    unsigned idr[RS_MAXR];
     if (s_long) {
-        // long runs of equal depth (e.g. a flat layer facing the camera): full LSD on (key, id): id digits first
-        __syncthreads();
+        // long runs of equal depth (e.g. a flat layer facing the camera): full LSD on (key, id) from the bucket
+        // order: the id digits first (the ids themselves serve as the keys), then the depth digits
 #pragma unroll
         for (int r = 0; r < RS_MAXR; r++) {
-            if (r < R) {
-                const int e = c0 + r * 64 + lane;
-                if (e < n) { kr[r] = sk[e]; vr[r] = sv[e]; }
-            }
+            const int e = c0 + r * 64 + lane;
+            if (r < R && e < n) { kr[r] = (unsigned)seg[e]; pr[r] = (unsigned short)e; }
         }
-        __syncthreads();
-        vmax = wave_max_u32(vmax);
-        if (lane == 0) atomicMax(&s_max, 0u);  // keep s_max; vmax reduced below
-        __shared__ unsigned s_vmax;
-        if (tid == 0) s_vmax = 0u;
-        __syncthreads();
-        if (lane == 0) atomicMax(&s_vmax, vmax);
-        __syncthreads();
-        const int vpasses = s_vmax ? (32 - __clz(s_vmax) + 7) >> 3 : 0;
-        const int total = vpasses + kpasses;
-        for (int p = 0; p < total; p++) {
-            const bool byv = p < vpasses;
-            radix_pass(kr, vr, byv, 8 * (byv ? p : p - vpasses), n, c0, R, sk, sv, cnt, s_wsum);
-            if (p + 1 < total) {
+        const int vbits = s_vmax ? 32 - __clz(s_vmax) : 0;
+        for (int sh = 0; sh < vbits; sh += RS_DBITS) {
+            radix_pass(kr, pr, sh, min(RS_DBITS, vbits - sh), n, c0, R, sk, sp, cnt, s_wsum);
+            reload();
+        }
 #pragma unroll
-                for (int r = 0; r < RS_MAXR; r++) {
-                    if (r < R) {
-                        const int e = c0 + r * 64 + lane;
-                        if (e < n) { kr[r] = sk[e]; vr[r] = sv[e]; }
+        for (int r = 0; r < RS_MAXR; r++) {
+            const int e = c0 + r * 64 + lane;
+            if (r < R && e < n) kr[r] = (unsigned)(seg[pr[r]] >> 32) - kmin;
+        }
+        for (int sh = 0; sh < kbits; sh += RS_DBITS) {
+            radix_pass(kr, pr, sh, min(RS_DBITS, kbits - sh), n, c0, R, sk, sp, cnt, s_wsum);
+            reload();
+        }
+#pragma unroll
+        for (int r = 0; r < RS_MAXR; r++) {
+            idr[r] = 0u;
+            const int e = c0 + r * 64 + lane;
+            if (r < R && e < n) idr[r] = (unsigned)seg[pr[r]];
+        }
+    } else {
+        // short runs (<= 32): gather the ids in key order, then order each run of equal keys by id
+#pragma unroll
+        for (int r = 0; r < RS_MAXR; r++) {
+            idr[r] = 0u;
+            const int e = c0 + r * 64 + lane;
+            if (r < R && e < n) idr[r] = (unsigned)seg[sp[e]];
+        }
+        bool any_tie = false;
+        for (int q = tid; q + 1 < n; q += RS_THREADS) any_tie |= sk[q] == sk[q + 1];
+        if (__syncthreads_or(any_tie)) {
+            unsigned *ids_l = reinterpret_cast<unsigned *>(sp);  // sp + cnt = RS_CAP u32, free after the gather
+#pragma unroll
+            for (int r = 0; r < RS_MAXR; r++) {
+                const int e = c0 + r * 64 + lane;
+                if (r < R && e < n) ids_l[e] = idr[r];
+            }
+            __syncthreads();
+            for (int q = tid; q < n; q += RS_THREADS) {
+                if (q + 1 < n && sk[q] == sk[q + 1] && (q == 0 || sk[q - 1] != sk[q])) {
+                    int e = q + 1;
+                    while (e < n && sk[e] == sk[q]) e++;
+                    for (int a2 = q + 1; a2 < e; a2++) {
+                        const unsigned v = ids_l[a2];
+                        int z = a2 - 1;
+                        while (z >= q && ids_l[z] > v) { ids_l[z + 1] = ids_l[z]; z--; }
+                        ids_l[z + 1] = v;
                     }
                 }
             }
-        }
-    } else {
-        // short runs: insertion-sort each run by id (runs <= 32 long)
-        for (int q = tid; q < n; q += RS_THREADS) {
-            if (q + 1 < n && sk[q] == sk[q + 1] && (q == 0 || sk[q - 1] != sk[q])) {
-                int e = q + 1;
-                while (e < n && sk[e] == sk[q]) e++;
-                for (int a = q + 1; a < e; a++) {
-                    const unsigned v = sv[a];
-                    int z = a - 1;
-                    while (z >= q && sv[z] > v) { sv[z + 1] = sv[z]; z--; }
-                    sv[z + 1] = v;
-                }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < RS_MAXR; r++) {
+                const int e = c0 + r * 64 + lane;
+                if (r < R && e < n) idr[r] = ids_l[e];
             }
         }
-        __syncthreads();
     }
+    __syncthreads();  // every read of the bucket (seg) is done before the ids overwrite it in place
     unsigned *ids = reinterpret_cast<unsigned *>(seg);
-    for (int q = tid; q < n; q += RS_THREADS) ids[q] = sv[q];
+#pragma unroll
+    for (int r = 0; r < RS_MAXR; r++) {
+        const int e = c0 + r * 64 + lane;
+        if (r < R && e < n) ids[e] = idr[r];
+    }
+}
+
+// k_sort: grid (B*V*T), block RS_THREADS, dynamic LDS RS_LDS bytes.
+__global__ __launch_bounds__(RS_THREADS) void k_sort(long long slot_stride, const int *__restrict__ tile_start,
+                                                     const int *__restrict__ tile_count,
+                                                     unsigned long long *__restrict__ pairs,
+                                                     unsigned long long *__restrict__ counters) {
+    long long base;
+    int n;
+    tile_range(blockIdx.x, slot_stride, tile_start, tile_count, base, n);
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    if (counters && threadIdx.x == 0) {  // per-workgroup timeline + bucket size (see lgm_render_debug_counters)
+        counters[8 + 8 * (size_t)blockIdx.x + 4] = t_start;
+        counters[8 + 8 * (size_t)blockIdx.x + 6] = (unsigned long long)n;
+    }
+    sort_tile(base, n, pairs);
+    if (counters) {
+        __syncthreads();
+        if (threadIdx.x == 0) counters[8 + 8 * (size_t)blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 }  // namespace
@@ -491,17 +641,18 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     uint2 *rects = (uint2 *)(ws + L.rects);
     int *tcount = (int *)(ws + L.tile_count), *tstart = (int *)(ws + L.tile_start);
     unsigned long long *pairs = (unsigned long long *)(ws + L.pairs), *misc = (unsigned long long *)(ws + L.misc);
-    const size_t lds = d.T <= LDS_HIST_MAX ? 2 * (size_t)d.T * 4 : 0;
+    float *accum = (float *)(ws + L.accum);
+    const size_t lds = d.T <= LDS_HIST_MAX ? 3 * (size_t)d.T * 4 : 0;
     dim3 grid((d.N + BIN_G - 1) / BIN_G, d.BV);
     if (d.N > 0) {
         if (count_only || !L.slot) {
-            LGM_LAUNCH("k_bin_count", st, (k_bin<COUNT><<<grid, 256, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
-                       gA, gB, gD, rects, nullptr, tcount, tstart, pairs, 0, misc)));
+            LGM_LAUNCH("k_bin_count", st, (k_bin<COUNT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
+                       gA, gB, gD, rects, nullptr, tcount, tstart, pairs, 0, misc, accum)));
         }
         if (!count_only) {
             if (L.slot) {
-                LGM_LAUNCH("k_bin", st, (k_bin<EMIT_SLOT><<<grid, 256, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
-                           gA, gB, gD, rects, radii_out, tcount, tstart, pairs, (long long)d.N, misc)));
+                LGM_LAUNCH("k_bin", st, (k_bin<EMIT_SLOT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
+                           gA, gB, gD, rects, radii_out, tcount, tstart, pairs, (long long)d.N, misc, accum)));
             } else {
                 LGM_LAUNCH("k_scan", st, (k_scan<<<1, 1024, 0, st>>>(tcount, (int)M, tstart)));
                 if (hipMemsetAsync(ws + L.tile_count, 0, M * 4, st) != hipSuccess ||
@@ -509,11 +660,11 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                     set_error("hipMemsetAsync failed");
                     return LGM_E_HIP;
                 }
-                LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, 256, lds, st>>>(d, gaussians, cam_view,
-                           cam_view_proj, gA, gB, gD, rects, radii_out, tcount, tstart, pairs, 0, misc)));
+                LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view,
+                           cam_view_proj, gA, gB, gD, rects, radii_out, tcount, tstart, pairs, 0, misc, accum)));
             }
             LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M, RS_THREADS, RS_LDS, st>>>(
-                                         L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs)));
+                                         L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs, d.counters)));
         }
     }
     if (stats_out && hipMemcpyAsync(stats_out, ws + L.misc, 16, hipMemcpyDeviceToDevice, st) != hipSuccess) {

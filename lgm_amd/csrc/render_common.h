@@ -25,7 +25,7 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 //   slot mode   (pair_capacity <= 0): tile (bv, t) owns pairs[(bv*T + t) * N, +N): no counting pass, no scan.
 //   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
 struct Layout {
-    size_t gA, gB, gD, rects, tile_count, tile_start, pairs, final_T, n_contrib, accum, misc, total;
+    size_t gA, gB, gD, rects, tile_count, tile_start, pairs, final_T, n_contrib, cmask, accum, misc, total;
     long long cap;
     bool slot;
 };
@@ -46,6 +46,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.pairs = take((size_t)L.cap * 8);
     L.final_T = take(BV * P * 4);
     L.n_contrib = take(BV * P * 4);
+    L.cmask = take(BV * P);
     L.accum = take(BV * N * NACC * 4);
     L.misc = take(64);
     L.total = o;
@@ -57,6 +58,7 @@ struct Dims {
     float tanx, tany, fx, fy, mod;
     unsigned long long *counters;  // optional device u64[8] work counters (see lgm_render_debug_counters), or null
     int flags;                     // LGM_RENDER_NO_CULL: bin upstream's full 3-sigma rects (no exact culling)
+    int options;                   // per-call LGM_RENDER_CLAMP_IMAGE
 };
 
 // ------------------------------------------------------------------------------------------------------------

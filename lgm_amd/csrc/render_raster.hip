@@ -109,7 +109,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
                                                     const float *__restrict__ gD, const float *__restrict__ gauss,
                                                     const float *__restrict__ bg, float *__restrict__ out_img,
                                                     float *__restrict__ out_depth, float *__restrict__ out_alpha,
-                                                    float *__restrict__ final_T, int *__restrict__ n_contrib) {
+                                                    float *__restrict__ final_T, int *__restrict__ n_contrib,
+                                                    unsigned char *__restrict__ cmask) {
     __shared__ Stage S;
     const int tile = blockIdx.x;
     const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
@@ -187,8 +188,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
             atomicMax(&d.counters[7], (unsigned long long)c_iter);
         }
         if (tid == 0) {  // per-workgroup timeline (100 MHz s_memrealtime ticks): [8 + 4*tile] start, +1 end
-            d.counters[8 + 4 * (size_t)tile] = t_start;
-            d.counters[8 + 4 * (size_t)tile + 1] = __builtin_amdgcn_s_memrealtime();
+            d.counters[8 + 8 * (size_t)tile] = t_start;
+            d.counters[8 + 8 * (size_t)tile + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
     if (inside) {
@@ -197,9 +198,17 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
         final_T[bv * P + pid] = Tr;
         n_contrib[bv * P + pid] = last;
         float *img = out_img + (size_t)bv * 3 * P;
-        img[pid] = C0 + Tr * bg[0];
-        img[P + pid] = C1 + Tr * bg[1];
-        img[2 * P + pid] = C2 + Tr * bg[2];
+        float c0 = C0 + Tr * bg[0], c1 = C1 + Tr * bg[1], c2 = C2 + Tr * bg[2];
+        if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // core/gs.py:87, gradient mask kept for the backward
+            auto in01 = [](float v) { return (v >= 0.f && v <= 1.f) ? 1u : 0u; };
+            cmask[bv * P + pid] = (unsigned char)(in01(c0) | (in01(c1) << 1) | (in01(c2) << 2));
+            c0 = fminf(fmaxf(c0, 0.f), 1.f);
+            c1 = fminf(fmaxf(c1, 0.f), 1.f);
+            c2 = fminf(fmaxf(c2, 0.f), 1.f);
+        }
+        img[pid] = c0;
+        img[P + pid] = c1;
+        img[2 * P + pid] = c2;
         out_depth[bv * P + pid] = D;
         out_alpha[bv * P + pid] = 1 - Tr;
     }
@@ -227,7 +236,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_strid
                                                     const int *__restrict__ n_contrib,
                                                     const float *__restrict__ d_img,
                                                     const float *__restrict__ d_depth,
-                                                    const float *__restrict__ d_alpha, float *__restrict__ accum) {
+                                                    const float *__restrict__ d_alpha,
+                                                    const unsigned char *__restrict__ cmask,
+                                                    float *__restrict__ accum) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
     constexpr int LS = TILE_PIX + 1;             // padded LDS row stride (no bank conflicts)
     __shared__ Stage S;
@@ -256,6 +267,12 @@ __global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_strid
         dp0 = di[pid];
         dp1 = di[P + pid];
         dp2 = di[2 * P + pid];
+        if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // torch clamp gradient: passes where 0 <= x <= 1
+            const unsigned m = cmask[bv * P + pid];
+            dp0 = (m & 1u) ? dp0 : 0.f;
+            dp1 = (m & 2u) ? dp1 : 0.f;
+            dp2 = (m & 4u) ? dp2 : 0.f;
+        }
         if (DEPTH) dpd = d_depth[bv * P + pid];
         if (d_alpha) dpa = d_alpha[bv * P + pid];
     }
@@ -411,8 +428,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_strid
         }
     }
     if (d.counters && tid == 0) {
-        d.counters[8 + 4 * (size_t)tile + 2] = t_start;
-        d.counters[8 + 4 * (size_t)tile + 3] = __builtin_amdgcn_s_memrealtime();
+        d.counters[8 + 8 * (size_t)tile + 2] = t_start;
+        d.counters[8 + 8 * (size_t)tile + 3] = __builtin_amdgcn_s_memrealtime();
     }
     if (d.counters && lane == 0) {
         atomicAdd(&d.counters[2], (unsigned long long)c_iter);
@@ -426,7 +443,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_strid
 __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__restrict__ gauss,
                                                      const float *__restrict__ views,
                                                      const float *__restrict__ projs, const uint2 *__restrict__ rects,
-                                                     const float *__restrict__ accum, float *__restrict__ d_gauss,
+                                                     float *__restrict__ accum, float *__restrict__ d_gauss,
                                                      float *__restrict__ d_means2D) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
@@ -451,7 +468,15 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
             if (d_means2D) { d_means2D[2 * k] = 0.f; d_means2D[2 * k + 1] = 0.f; }
             continue;
         }
-        const float *acc = accum + k * NACC;
+        float2 *acc2 = reinterpret_cast<float2 *>(accum + k * NACC);
+        float acc[NACC];
+#pragma unroll
+        for (int q = 0; q < NACC / 2; q++) {  // read, then re-zero for the next backward over this workspace
+            const float2 a = acc2[q];
+            acc[2 * q] = a.x;
+            acc[2 * q + 1] = a.y;
+            acc2[q] = make_float2(0.f, 0.f);
+        }
         const float dm2x = acc[0], dm2y = acc[1];
         const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
         dop += acc[5];
@@ -557,17 +582,14 @@ int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, fl
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gA), (const float4 *)(ws + L.gB),
                                        (const float *)(ws + L.gD), gaussians, bg, image, depth, alpha,
-                                       (float *)(ws + L.final_T), (int *)(ws + L.n_contrib))));
+                                       (float *)(ws + L.final_T), (int *)(ws + L.n_contrib),
+                                       (unsigned char *)(ws + L.cmask))));
     return LGM_OK;
 }
 
 int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_view, const float *cam_view_proj,
                       const float *bg, const float *d_image, const float *d_depth, const float *d_alpha,
                       float *d_gaussians, float *d_means2D, char *ws, const Layout &L, hipStream_t st) {
-    if (hipMemsetAsync(ws + L.accum, 0, (size_t)d.BV * d.N * NACC * 4, st) != hipSuccess) {
-        set_error("hipMemsetAsync failed");
-        return LGM_E_HIP;
-    }
     auto bwd = d_depth ? k_render_bwd<true> : k_render_bwd<false>;
     LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.tile_start),
@@ -575,11 +597,12 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
                                        (const float4 *)(ws + L.gA), (const float4 *)(ws + L.gB),
                                        (const float *)(ws + L.gD), gaussians, bg, (const float *)(ws + L.final_T),
                                        (const int *)(ws + L.n_contrib), d_image, d_depth, d_alpha,
+                                       (const unsigned char *)(ws + L.cmask),
                                        (float *)(ws + L.accum))));
     dim3 grid((d.N + 255) / 256, d.B);
     LGM_LAUNCH("k_preproc_bwd", st, (k_preproc_bwd<<<grid, 256, 0, st>>>(d, gaussians, cam_view, cam_view_proj,
                                                                         (const uint2 *)(ws + L.rects),
-                                                                        (const float *)(ws + L.accum), d_gaussians,
+                                                                        (float *)(ws + L.accum), d_gaussians,
                                                                         d_means2D)));
     return LGM_OK;
 }

@@ -29,7 +29,7 @@ class _RasterizeBatched(torch.autograd.Function):
     """Autograd Function over all B x V renders (replaces B*V applications of the EXT _RasterizeGaussians)."""
 
     @staticmethod
-    def forward(ctx, g, cam_view, cam_view_proj, bg, tanx, tany, scale_modifier, H, W):
+    def forward(ctx, g, cam_view, cam_view_proj, bg, tanx, tany, scale_modifier, H, W, options):
         L = _native.lib()
         B, N = g.shape[0], g.shape[1]
         V = cam_view.shape[1]
@@ -56,17 +56,18 @@ class _RasterizeBatched(torch.autograd.Function):
         _native.check(L.lgm_render_forward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
                                            _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
                                            _native.ptr(image), _native.ptr(depth), _native.ptr(alpha), None,
-                                           _native.ptr(ws), ws_bytes, cap, None, stream), "lgm_render_forward")
+                                           _native.ptr(ws), ws_bytes, cap, None, options, stream),
+                      "lgm_render_forward")
         ctx.save_for_backward(g, cam_view, cam_view_proj, bg)
         ctx.set_materialize_grads(False)  # unused outputs (LGM never uses depth) arrive as None, not zeros
         ctx.ws, ctx.ws_bytes, ctx.cap = ws, ws_bytes, cap
-        ctx.params = (tanx, tany, scale_modifier, H, W)
+        ctx.params = (tanx, tany, scale_modifier, H, W, options)
         return image, depth, alpha
 
     @staticmethod
     def backward(ctx, d_image, d_depth, d_alpha):
         g, cam_view, cam_view_proj, bg = ctx.saved_tensors
-        tanx, tany, scale_modifier, H, W = ctx.params
+        tanx, tany, scale_modifier, H, W, options = ctx.params
         B, N = g.shape[0], g.shape[1]
         V = cam_view.shape[1]
         if d_image is None:
@@ -80,12 +81,13 @@ class _RasterizeBatched(torch.autograd.Function):
                                             _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
                                             _native.ptr(d_image), _native.ptr(d_depth), _native.ptr(d_alpha),
                                             _native.ptr(d_g), None, _native.ptr(ctx.ws), ctx.ws_bytes, ctx.cap,
-                                            _native.stream_of(g.device)), "lgm_render_backward")
-        return d_g, None, None, None, None, None, None, None, None
+                                            options, _native.stream_of(g.device)), "lgm_render_backward")
+        return d_g, None, None, None, None, None, None, None, None, None
 
 
-def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, scale_modifier=1.0):
-    """Functional form: returns (image [B,V,3,H,W] UNCLAMPED, depth [B,V,1,H,W], alpha [B,V,1,H,W])."""
+def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, scale_modifier=1.0, clamp=False):
+    """Functional form: returns (image [B,V,3,H,W], depth [B,V,1,H,W], alpha [B,V,1,H,W]). The image is
+    unclamped unless clamp=True, which applies core/gs.py:87's clamp(0, 1) (and its gradient) inside the kernels."""
     for t, n in ((gaussians, "gaussians"), (cam_view, "cam_view"), (cam_view_proj, "cam_view_proj")):
         _native.require_device_tensor(t, n)
     g = gaussians.float().contiguous()
@@ -98,7 +100,7 @@ def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, sc
     if cv.shape[:2] != cvp.shape[:2] or cv.shape[0] != g.shape[0] or cv.shape[-2:] != (4, 4):
         raise ValueError("cam_view / cam_view_proj must be [B,V,4,4] with B matching gaussians")
     return _RasterizeBatched.apply(g, cv, cvp, bgt, float(tanfovx), float(tanfovy), float(scale_modifier),
-                                   int(H), int(W))
+                                   int(H), int(W), _native.RENDER_CLAMP_IMAGE if clamp else 0)
 
 
 def count_pairs(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scale_modifier=1.0):
@@ -141,8 +143,9 @@ class GaussianRenderer:
         S = int(self.opt.output_size)
         bg = self.bg_color if bg_color is None else bg_color
         tan = float(self.tan_half_fov)
-        image, depth, alpha = rasterize(gaussians, cam_view, cam_view_proj, bg, tan, tan, S, S, scale_modifier)
-        image = image.clamp(0, 1)  # core/gs.py:87
+        # core/gs.py:87's clamp(0, 1) and its gradient are applied inside the kernels
+        image, depth, alpha = rasterize(gaussians, cam_view, cam_view_proj, bg, tan, tan, S, S, scale_modifier,
+                                        clamp=True)
         return {"image": image, "alpha": alpha, "depth": depth}
 
     def save_ply(self, gaussians, path, compatible=True):

@@ -16,7 +16,8 @@ g = synthetic_gaussians(1, 100000, seed=1).to(dev).requires_grad_(True)
 cv, cvp, cp = orbit_cameras(6)
 d_img, _, d_alpha, bg = synthetic_upstream_grads(1, 6, 256, 256, seed=1001)
 M = 6 * 256
-cnt = torch.zeros(8 + 4 * M, dtype=torch.int64, device=dev)
+NB = 6 * ((100000 + 1023) // 1024)  # k_bin workgroups (1024 Gaussians each)
+cnt = torch.zeros(8 + 8 * M + 8 * NB + 4096, dtype=torch.int64, device=dev)
 L = _native.lib()
 L.lgm_render_debug_counters(_native.ptr(cnt))
 out = r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev), bg_color=bg.to(dev))
@@ -28,8 +29,13 @@ names = ["fwd_wave_iters", "fwd_contribs", "bwd_wave_iters", "bwd_contribs", "bw
          "fwd_entries_staged", "fwd_max_wave_iters"]
 res = dict(zip(names, c[:8]))
 import numpy as np  # noqa: E402
-tl = np.array(c[8:], dtype=np.int64).reshape(M, 4)
-for name, (a, b) in {"fwd": (0, 1), "bwd": (2, 3)}.items():
+tl = np.array(c[8:8 + 8 * M], dtype=np.int64).reshape(M, 8)
+nl = tl[:, 6]
+res["tile_list_max"] = int(nl.max())
+res["tile_list_p50"] = float(np.median(nl))
+res["tile_list_mean"] = float(nl.mean())
+res["tile_list_hist_1k"] = np.bincount(nl // 1024).tolist()
+for name, (a, b) in {"fwd": (0, 1), "bwd": (2, 3), "sort": (4, 5)}.items():
     st, en = tl[:, a], tl[:, b]
     ok = en > 0
     st, en = st[ok], en[ok]
@@ -47,4 +53,29 @@ res["fwd_lane_util"] = c[1] / max(1, 64 * c[0])
 res["bwd_lane_util"] = c[3] / max(1, 64 * c[2])
 print(json.dumps(res, indent=1))
 os.makedirs("gpurun_out", exist_ok=True)
+json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)
+st, en = tl[:, 4], tl[:, 5]
+ok = en > 0
+dur = (en - st) * 0.01
+res2 = {}
+for k in range(int(nl.max()) // 512 + 1):
+    m = ok & (nl // 512 == k)
+    if m.any():
+        res2[f"{512 * k}-{512 * k + 511}"] = [int(m.sum()), round(float(dur[m].mean()), 2), round(float(dur[m].max()), 2)]
+print("sort us by list length [tiles, mean, max]:", json.dumps(res2))
+res["sort_us_by_n"] = res2
+json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)
+
+bt = np.array(c[8 + 8 * M: 8 + 8 * M + 8 * NB], dtype=np.int64).reshape(NB, 8)
+ok = bt[:, 4] > 0
+bt = bt[ok]
+t0 = bt[:, 0].min()
+ph = {"preproc": (0, 1), "sort+tests": (1, 2), "reserve+scan": (2, 3), "emit": (3, 4), "total": (0, 4)}
+binres = {k: [round(float(np.median((bt[:, b] - bt[:, a]) * 0.01)), 2), round(float(((bt[:, b] - bt[:, a]) * 0.01).max()), 2)]
+          for k, (a, b) in ph.items()}
+binres["span_us"] = round(float((bt[:, 4].max() - t0) * 0.01), 2)
+binres["start_spread_us"] = round(float((bt[:, 0].max() - t0) * 0.01), 2)
+binres["hits_median"] = float(np.median(bt[:, 5]))
+print("k_bin phases [median us, max us]:", json.dumps(binres))
+res["k_bin_phases"] = binres
 json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)

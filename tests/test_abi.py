@@ -31,12 +31,16 @@ def test_library_exports_all_declared_symbols():
 
 def test_workspace_and_errors():
     L = _native.lib()
-    assert L.lgm_abi_version() == 1
+    assert L.lgm_abi_version() == _native.ABI_VERSION
     w1 = L.lgm_render_workspace_size(1, 6, 100000, 256, 256, 0)
     w2 = L.lgm_render_workspace_size(1, 6, 100000, 256, 256, 1000000)
     assert w1 > w2 > 0
     assert L.lgm_render_workspace_size(0, 6, 10, 256, 256, 0) == 0
     # invalid arguments are reported, never thrown
     rc = L.lgm_render_forward(1, 1, 10, 16, 16, None, None, None, None, 1.0, 1.0, 1.0, None, None, None, None, None,
-                              0, 0, None, None)
+                              0, 0, None, 0, None)
     assert rc < 0 and b"null" in L.lgm_last_error()
+    # attention: unsupported head dim / dtype are reported, never thrown
+    rc = L.lgm_attn_forward(1, 1, 16, 2, 48, 0.1, None, None, None, 0, None, None, None)
+    assert rc < 0 and b"D must be" in L.lgm_last_error()
+    assert L.lgm_attn_workspace_size(1, 2, 100, 4) == 2 * 100 * 4 * 4

@@ -191,3 +191,28 @@ def test_exact_culling_is_output_preserving(cuda):
     for k in ("image", "depth", "alpha"):
         assert np.array_equal(full[k], culled[k]), k
     assert rel_l2(culled["d_gaussians"], full["d_gaussians"]) < 1e-5
+
+
+def test_fused_clamp_matches_torch_clamp(cuda):
+    """LGM_RENDER_CLAMP_IMAGE == core/gs.py:87's image.clamp(0, 1) and its autograd: the forward equals clamp of
+    the unclamped image bitwise, the gradient equals the unclamped path fed torch's clamp mask (inclusive)."""
+    g, cv, cvp = scene(B=2, N=3000, V=2, seed=33)
+    g[..., 11:14] = g[..., 11:14] * 2.2 - 0.6  # colours outside [0, 1] so both clamp bounds are hit
+    d_img, _, d_alp, bg = upstream(2, 2, 64, 64)
+    outs = {}
+    for clamp in (False, True):
+        gd = g.to(cuda).requires_grad_(True)
+        img, _, alp = rasterize(gd, cv.to(cuda), cvp.to(cuda), bg.to(cuda), TAN, TAN, 64, 64, clamp=clamp)
+        if clamp:
+            up = d_img.to(cuda)
+        else:
+            raw = img.detach()
+            outs["raw"] = raw
+            up = d_img.to(cuda) * ((raw >= 0) & (raw <= 1)).float()
+        ((img * up).sum() + (alp * d_alp.to(cuda)).sum()).backward()
+        outs[clamp] = (img.detach(), gd.grad.clone())
+    raw = outs["raw"]
+    frac = float(((raw < 0) | (raw > 1)).float().mean())
+    assert 0.01 < frac < 0.9, frac  # the clamp is actually exercised
+    assert torch.equal(outs[True][0], raw.clamp(0, 1))
+    assert rel_l2(outs[True][1].cpu().numpy(), outs[False][1].cpu().numpy()) < 1e-5

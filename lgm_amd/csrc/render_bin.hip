@@ -277,6 +277,46 @@ __global__ __launch_bounds__(1024) void k_scan(const int *__restrict__ count, in
     if (tid == 1023) start[M] = (int)wsum[15];
 }
 
+// k_order: one workgroup; the (view, tile) work items sorted by decreasing bucket size (counting sort on
+// n / 8). The compositing kernels take their tiles in this order, so the longest lists start first and the
+// short ones fill the gaps (longest-processing-time-first scheduling).
+constexpr int ORD_THREADS = 1024, ORD_BK = 2048;
+__global__ __launch_bounds__(ORD_THREADS) void k_order(int M, long long slot_stride, const int *__restrict__ tile_start,
+                                                       const int *__restrict__ tile_count, int *__restrict__ order) {
+    __shared__ int hist[ORD_BK];
+    __shared__ int s_wsum[ORD_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int q = tid; q < ORD_BK; q += ORD_THREADS) hist[q] = 0;
+    __syncthreads();
+    auto key = [&](int t) {
+        long long base;
+        int n;
+        tile_range(t, slot_stride, tile_start, tile_count, base, n);
+        return ORD_BK - 1 - min(n >> 3, ORD_BK - 1);  // descending size
+    };
+    for (int t = tid; t < M; t += ORD_THREADS) atomicAdd(&hist[key(t)], 1);
+    __syncthreads();
+    // exclusive scan of ORD_BK counters, ORD_BK / ORD_THREADS per thread
+    constexpr int PER = ORD_BK / ORD_THREADS;
+    int loc[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; j++) { loc[j] = hist[tid * PER + j]; sum += loc[j]; }
+    int x = sum;
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+        const int y = __shfl_up(x, dd, 64);
+        if (lane >= dd) x += y;
+    }
+    if (lane == 63) s_wsum[w] = x;
+    __syncthreads();
+    int run = x - sum;
+    for (int ww = 0; ww < w; ww++) run += s_wsum[ww];
+#pragma unroll
+    for (int j = 0; j < PER; j++) { hist[tid * PER + j] = run; run += loc[j]; }
+    __syncthreads();
+    for (int t = tid; t < M; t += ORD_THREADS) order[atomicAdd(&hist[key(t)], 1)] = t;
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Per-tile sort: RS_CAP entries sorted in LDS (larger buckets take sort_oversized): u32 keys, u16 bucket positions
 // and per-wave 512-bucket counters (40 KB at 512 threads; 8 rows per lane keep it at ~90 VGPRs).
@@ -666,6 +706,14 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
             LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M, RS_THREADS, RS_LDS, st>>>(
                                          L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs, d.counters)));
         }
+    }
+    if (d.N == 0 && !L.slot && hipMemsetAsync(ws + L.tile_start, 0, (M + 1) * 4, st) != hipSuccess) {
+        set_error("hipMemsetAsync failed");  // packed mode with no Gaussians: every tile range is empty
+        return LGM_E_HIP;
+    }
+    if (!count_only) {  // also for N == 0: the compositing kernels index their tiles through it
+        LGM_LAUNCH("k_order", st, (k_order<<<1, ORD_THREADS, 0, st>>>((int)M, L.slot ? (long long)d.N : -1LL,
+                                                                     tstart, tcount, (int *)(ws + L.order))));
     }
     if (stats_out && hipMemcpyAsync(stats_out, ws + L.misc, 16, hipMemcpyDeviceToDevice, st) != hipSuccess) {
         set_error("hipMemcpyAsync failed");

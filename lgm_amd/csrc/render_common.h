@@ -25,7 +25,7 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 //   slot mode   (pair_capacity <= 0): tile (bv, t) owns pairs[(bv*T + t) * N, +N): no counting pass, no scan.
 //   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
 struct Layout {
-    size_t gA, gB, gD, rects, tile_count, tile_start, pairs, final_T, n_contrib, cmask, accum, misc, total;
+    size_t gA, gB, gD, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, cmask, accum, misc, total;
     long long cap;
     bool slot;
 };
@@ -43,6 +43,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.rects = take(BV * N * 8);
     L.tile_count = take(BV * T * 4);
     L.tile_start = take((BV * T + 1) * 4);
+    L.order = take(BV * T * 4);
     L.pairs = take((size_t)L.cap * 8);
     L.final_T = take(BV * P * 4);
     L.n_contrib = take(BV * P * 4);

@@ -12,6 +12,9 @@
 #ifndef LGM_BWD_BU
 #define LGM_BWD_BU 2  // backward entries evaluated per step (ILP vs registers)
 #endif
+#ifndef LGM_BWD_MFMA
+#define LGM_BWD_MFMA 1  // per-entry gradient sums as pixel moments on the f32 MFMA (else DPP row sums)
+#endif
 
 namespace lgm {
 namespace {
@@ -33,6 +36,10 @@ __device__ __forceinline__ int wave_max_i32(int v) {
 
 // Stage entries [b0, b0 + 256) of the tile's list (fwd: front-to-back; bwd: reversed) and build the per-wave
 // compacted lists. Returns this wave's list length.
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+constexpr int WU_LD = 66;  // row stride of the per-wave [16 columns][64 pixels] gradient image (conflict-free)
+constexpr int MB = 8;      // entries per moment-MFMA batch (columns 0..7: w, 8..15: u)
+
 constexpr int SENT = TILE_PIX;  // sentinel slot: opacity 0, never contributes (pads the per-wave lists)
 struct Stage {
     float4 P[TILE_PIX + 1];  // x, y, A, B
@@ -102,7 +109,8 @@ __device__ __forceinline__ void init_sentinel(Stage &S) {
 }
 
 // k_render_fwd: grid (B*V*T), block 256.
-__global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_stride, const int *__restrict__ tile_start,
+__global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_stride, const int *__restrict__ order,
+                                                    const int *__restrict__ tile_start,
                                                     const int *__restrict__ tile_count,
                                                     const unsigned long long *__restrict__ pairs,
                                                     const float4 *__restrict__ gA, const float4 *__restrict__ gB,
@@ -112,7 +120,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
                                                     float *__restrict__ final_T, int *__restrict__ n_contrib,
                                                     unsigned char *__restrict__ cmask) {
     __shared__ Stage S;
-    const int tile = blockIdx.x;
+    const int tile = order[blockIdx.x];  // longest lists first (k_order)
     const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
     const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -226,8 +234,12 @@ __device__ __forceinline__ float row_sum16(float v) {
 }
 
 // k_render_bwd: grid (B*V*T), block 256. DEPTH: an upstream depth gradient is present (LGM passes none).
+#ifndef LGM_BWD_WPE
+#define LGM_BWD_WPE 3  // minimum waves per SIMD the register allocation must allow (4: <= 128 VGPRs)
+#endif
 template <bool DEPTH>
-__global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_stride, const int *__restrict__ tile_start,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE))) void k_render_bwd(Dims d, long long slot_stride, const int *__restrict__ order,
+                                                    const int *__restrict__ tile_start,
                                                     const int *__restrict__ tile_count,
                                                     const unsigned long long *__restrict__ pairs,
                                                     const float4 *__restrict__ gA, const float4 *__restrict__ gB,
@@ -244,7 +256,11 @@ __global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_strid
     __shared__ Stage S;
     __shared__ float sAcc[LS * NACC];
     __shared__ int sMaxLast;
-    const int tile = blockIdx.x;
+#if LGM_BWD_MFMA
+    __shared__ float sWU[4][16 * WU_LD];
+    __shared__ unsigned short sBidx[4][MB];
+#endif
+    const int tile = order[blockIdx.x];  // longest lists first (k_order)
     const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
     const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -294,6 +310,72 @@ __global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_strid
     const int ql = lane & 15;
     constexpr int BU = LGM_BWD_BU;
     unsigned c_iter = 0, c_valid = 0, c_dense = 0, c_sparse = 0;
+#if LGM_BWD_MFMA
+    // Every per-entry gradient sum over the wave's 64 pixels is a pixel moment of two per-(pixel, entry) scalars,
+    // w = G dL/dG and u = alpha T: sum_p w f(p) for f in {1, x, y, x^2, xy, y^2} (tile-centred pixel
+    // coordinates; mean2D and conic partials follow from these and the Gaussian centre) and sum_p u dL/dC_c(p).
+    // So the reduction is the product [features x pixels] . [pixels x entries]: MB entries' w (columns 0..MB-1)
+    // and u (columns MB..) are written to a per-wave LDS image and summed by 16 exact-f32 v_mfma_f32_16x16x4_f32
+    // over the 64 pixels. A operand: lane (ql, qk) holds feature ql of wave pixel 4s + qk, s = 0..15.
+    const int qk = lane >> 4;
+    const float cxT = (float)tx0 + 7.5f, cyT = (float)ty0 + 7.5f;
+    float *myWU = sWU[w];
+    myWU[lane] = dp0;
+    myWU[64 + lane] = dp1;
+    myWU[128 + lane] = dp2;
+    myWU[192 + lane] = dpd;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    float Af[16];
+#pragma unroll
+    for (int s4 = 0; s4 < 16; s4++) {
+        const int p = 4 * s4 + qk;
+        int lx2, ly2;
+        tile_pixel(w * 64 + p, lx2, ly2);
+        const float fx = (float)(tx0 + lx2) - cxT, fy = (float)(ty0 + ly2) - cyT;
+        float f = 0.f;
+        if (ql == 0) f = 1.f;
+        else if (ql == 1) f = fx;
+        else if (ql == 2) f = fy;
+        else if (ql == 3) f = fx * fx;
+        else if (ql == 4) f = fx * fy;
+        else if (ql == 5) f = fy * fy;
+        else if (ql <= 9) f = myWU[(ql - 6) * 64 + p];
+        Af[s4] = f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    auto flush_batch = [&](int nb) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 16; s4++)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[s4], myWU[ql * WU_LD + 4 * s4 + qk], acc, 0, 0, 0);
+        // D[row = 4 qk + r][col = ql]: moments 0..5 in w columns, rows 6..9 in u columns
+        if (ql < MB) {
+            if (ql < nb) {
+                const int e = sBidx[w][ql];
+                if (qk == 0) {
+                    atomicAdd(&sAcc[0 * LS + e], acc[0]);
+                    atomicAdd(&sAcc[1 * LS + e], acc[1]);
+                    atomicAdd(&sAcc[2 * LS + e], acc[2]);
+                    atomicAdd(&sAcc[3 * LS + e], acc[3]);
+                } else if (qk == 1) {
+                    atomicAdd(&sAcc[4 * LS + e], acc[0]);
+                    atomicAdd(&sAcc[5 * LS + e], acc[1]);
+                }
+            }
+        } else if (ql - MB < nb) {
+            const int e = sBidx[w][ql - MB];
+            if (qk == 1) {
+                atomicAdd(&sAcc[6 * LS + e], acc[2]);
+                atomicAdd(&sAcc[7 * LS + e], acc[3]);
+            } else if (qk == 2) {
+                atomicAdd(&sAcc[8 * LS + e], acc[0]);
+                if (DEPTH) atomicAdd(&sAcc[9 * LS + e], acc[1]);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    };
+#endif
 
     for (int b0 = 0; b0 < nlist; b0 += TILE_PIX) {
         __syncthreads();
@@ -308,12 +390,70 @@ __global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_strid
         c_iter += cnt;
         // BU entries per step: G, alpha and the G-derivatives are independent of the per-pixel recurrences, so
         // they are evaluated together (ILP); the T / suffix-accumulator recurrences stay serial in list order.
+#if LGM_BWD_MFMA
+        int nb = 0;  // entries in the pending MFMA batch (wave-uniform)
+#endif
         for (int kk = 0; kk < cnt; kk += BU) {
             int jj4[4];
             list4(S, w, kk & ~3, jj4);
             int jj[BU];
 #pragma unroll
             for (int u = 0; u < BU; u++) jj[u] = jj4[(kk & 3) + u];
+#if LGM_BWD_MFMA
+            float al[BU], Gv[BU], Gg[BU], inv[BU];
+            float4 cc[BU];
+            float v[BU][2];  // w = G dL/dG, u = alpha T
+#pragma unroll
+            for (int u = 0; u < BU; u++) {
+                const int pos = nlist - 1 - (b0 + jj[u]);  // 0-based position in the tile list
+                const float4 Pj = S.P[jj[u]];
+                const float2 Q = S.Q[jj[u]];
+                cc[u] = S.R[jj[u]];
+                const float dx = Pj.x - pfx, dy = Pj.y - pfy;
+                const float power = -0.5f * (Pj.z * dx * dx + Q.x * dy * dy) - Pj.w * dx * dy;
+                const float G = __builtin_amdgcn_exp2f(power * LOG2E);
+                const float alpha = fminf(0.99f, Q.y * G);
+                const bool ok = pos < last && power <= 0.0f && alpha >= 1.0f / 255.0f;
+                al[u] = ok ? alpha : 0.f;
+                Gv[u] = Q.y;  // opacity: dL/dG = opacity * dL/dopa
+                Gg[u] = G;
+                // 1 / (1 - alpha): v_rcp_f32 + one Newton step (~0.5 ulp, like the IEEE division upstream uses)
+                const float om = 1.f - alpha;
+                float r = __builtin_amdgcn_rcpf(om);
+                inv[u] = fmaf(fmaf(-om, r, 1.0f), r, r);
+            }
+#pragma unroll
+            for (int u = 0; u < BU; u++) {
+                v[u][0] = 0.f;
+                v[u][1] = 0.f;
+                if (al[u] == 0.f) continue;
+                const float alpha = al[u];
+                const float4 c = cc[u];
+                Tr = Tr * inv[u];
+                float dL_dopa = 0.f;
+                acc_r0 = last_alpha * lc0 + (1.f - last_alpha) * acc_r0;
+                lc0 = c.x;
+                dL_dopa += (c.x - acc_r0) * dp0;
+                acc_r1 = last_alpha * lc1 + (1.f - last_alpha) * acc_r1;
+                lc1 = c.y;
+                dL_dopa += (c.y - acc_r1) * dp1;
+                acc_r2 = last_alpha * lc2 + (1.f - last_alpha) * acc_r2;
+                lc2 = c.z;
+                dL_dopa += (c.z - acc_r2) * dp2;
+                if (DEPTH) {
+                    acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
+                    last_depth = c.w;
+                    dL_dopa += (c.w - acc_d) * dpd;
+                }
+                acc_a = last_alpha + (1.f - last_alpha) * acc_a;
+                dL_dopa += (1 - acc_a) * dpa;
+                dL_dopa *= Tr;
+                last_alpha = alpha;
+                dL_dopa += (-T_final * inv[u]) * bg_dot;
+                v[u][0] = Gg[u] * (Gv[u] * dL_dopa);
+                v[u][1] = alpha * Tr;  // dchannel_dcolor
+            }
+#else
             float al[BU], Gv[BU], ex[BU], ey[BU], inv[BU];
             float4 cc[BU];
             float v[BU][NACC];
@@ -389,6 +529,52 @@ __global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_strid
                 v[u][4] *= dL_dG;
                 v[u][5] *= dL_dopa;
             }
+#endif
+#if LGM_BWD_MFMA
+#pragma unroll
+            for (int u = 0; u < BU; u++) {
+                const bool valid = al[u] != 0.f;
+                const unsigned long long bal = __ballot(valid);  // wave-uniform
+                if (bal == 0ull) continue;
+                c_valid += __popcll(bal);
+                myWU[nb * WU_LD + lane] = valid ? v[u][0] : 0.f;        // w
+                myWU[(MB + nb) * WU_LD + lane] = valid ? v[u][1] : 0.f; // u
+                if (lane == 0) sBidx[w][nb] = (unsigned short)jj[u];
+                if (++nb == MB) {
+                    c_dense++;
+                    flush_batch(MB);
+                    nb = 0;
+                }
+            }
+        }
+        if (nb) {
+            c_sparse++;
+            flush_batch(nb);
+            nb = 0;
+        }
+        __syncthreads();
+        // moments -> gradient partials, in place (one thread per staged entry)
+        if (b0 + tid < nlist) {
+            const int j = tid;
+            const float4 Pj = S.P[j];
+            const float2 Qj = S.Q[j];
+            const float xg = Pj.x - cxT, yg = Pj.y - cyT;
+            float q[NACC];
+#pragma unroll
+            for (int qq = 0; qq < NACC; qq++) q[qq] = sAcc[qq * LS + j];
+            const float Sx = fmaf(xg, q[0], -q[1]), Sy = fmaf(yg, q[0], -q[2]);
+            const float Sxx = fmaf(xg, fmaf(xg, q[0], -2.f * q[1]), q[3]);
+            const float Sxy = fmaf(xg, fmaf(yg, q[0], -q[2]), fmaf(-yg, q[1], q[4]));
+            const float Syy = fmaf(yg, fmaf(yg, q[0], -2.f * q[2]), q[5]);
+            sAcc[0 * LS + j] = -ddelx_dx * (Pj.z * Sx + Pj.w * Sy);
+            sAcc[1 * LS + j] = -ddely_dy * (Qj.x * Sy + Pj.w * Sx);
+            sAcc[2 * LS + j] = -0.5f * Sxx;
+            sAcc[3 * LS + j] = -0.5f * Sxy;
+            sAcc[4 * LS + j] = -0.5f * Syy;
+            sAcc[5 * LS + j] = Qj.y > 0.f ? q[0] / Qj.y : 0.f;
+            // [6..9] colour / depth sums are already the partials
+        }
+#else
 #pragma unroll
             for (int u = 0; u < BU; u++) {
                 const bool valid = al[u] != 0.f;
@@ -414,6 +600,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(Dims d, long long slot_strid
                 }
             }
         }
+#endif
         __syncthreads();
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
@@ -578,7 +765,7 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
 int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, float *image, float *depth,
                       float *alpha, char *ws, const Layout &L, hipStream_t st) {
     LGM_LAUNCH("k_render_fwd", st, (k_render_fwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
-                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.tile_start),
+                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gA), (const float4 *)(ws + L.gB),
                                        (const float *)(ws + L.gD), gaussians, bg, image, depth, alpha,
@@ -592,7 +779,7 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
                       float *d_gaussians, float *d_means2D, char *ws, const Layout &L, hipStream_t st) {
     auto bwd = d_depth ? k_render_bwd<true> : k_render_bwd<false>;
     LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
-                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.tile_start),
+                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gA), (const float4 *)(ws + L.gB),
                                        (const float *)(ws + L.gD), gaussians, bg, (const float *)(ws + L.final_T),

@@ -13,13 +13,31 @@
 #define LGM_BWD_BU 2  // backward entries evaluated per step (ILP vs registers)
 #endif
 #ifndef LGM_BWD_MFMA
-#define LGM_BWD_MFMA 1  // per-entry gradient sums as pixel moments on the f32 MFMA (else DPP row sums)
+// per-entry gradient sums as pixel moments on the MFMA: 1 = exact-f32 16x16x4, 2 = split-bf16 16x16x32 (features
+// exact in bf16, w/u as hi + lo: ~2^-16 relative per product), 0 = DPP row sums
+#define LGM_BWD_MFMA 2
 #endif
 
 namespace lgm {
 namespace {
 
 __device__ __forceinline__ unsigned long long lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
+
+// Section stamps of the diagnostic build LGM_BWD_STAMPS (shares only: the stamps' waits change the schedule).
+#ifdef LGM_BWD_STAMPS
+__device__ __forceinline__ unsigned long long sec_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define SEC_T(v) const unsigned long long v = sec_stamp()
+#define SEC_ADD(acc, a, b) acc += (b) - (a)
+#else
+#define SEC_T(v)
+#define SEC_ADD(acc, a, b)
+#endif
 
 __device__ __forceinline__ int __reduce_add_wave(unsigned v) {
 #pragma unroll
@@ -37,7 +55,8 @@ __device__ __forceinline__ int wave_max_i32(int v) {
 // Stage entries [b0, b0 + 256) of the tile's list (fwd: front-to-back; bwd: reversed) and build the per-wave
 // compacted lists. Returns this wave's list length.
 typedef __attribute__((ext_vector_type(4))) float f32x4;
-constexpr int WU_LD = 66;  // row stride of the per-wave [16 columns][64 pixels] gradient image (conflict-free)
+constexpr int WU_LD = 68;  // row stride of the per-wave [16 columns][64 pixels] gradient image (16-B aligned rows)
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 constexpr int MB = 8;      // entries per moment-MFMA batch (columns 0..7: w, 8..15: u)
 
 constexpr int SENT = TILE_PIX;  // sentinel slot: opacity 0, never contributes (pads the per-wave lists)
@@ -254,7 +273,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
     constexpr int LS = TILE_PIX + 1;             // padded LDS row stride (no bank conflicts)
     __shared__ Stage S;
-    __shared__ float sAcc[LS * NACC];
+    __shared__ float sAcc[LS * NV];  // 9 rows without a depth gradient: 4 workgroups fit in the CU's LDS
     __shared__ int sMaxLast;
 #if LGM_BWD_MFMA
     __shared__ float sWU[4][16 * WU_LD];
@@ -310,6 +329,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
     const int ql = lane & 15;
     constexpr int BU = LGM_BWD_BU;
     unsigned c_iter = 0, c_valid = 0, c_dense = 0, c_sparse = 0;
+#ifdef LGM_BWD_STAMPS
+    unsigned long long sec_stage = 0, sec_compact = 0, sec_loop = 0, sec_flush = 0, sec_tail = 0;
+#endif
 #if LGM_BWD_MFMA
     // Every per-entry gradient sum over the wave's 64 pixels is a pixel moment of two per-(pixel, entry) scalars,
     // w = G dL/dG and u = alpha T: sum_p w f(p) for f in {1, x, y, x^2, xy, y^2} (tile-centred pixel
@@ -325,6 +347,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
     myWU[128 + lane] = dp2;
     myWU[192 + lane] = dpd;
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#if LGM_BWD_MFMA == 2
+    // A operand of v_mfma_f32_16x16x32_bf16: lane (ql, qk) holds feature ql of pixels 32 t + 8 qk + j, j = 0..7.
+    // The geometric features (half-integer tile coordinates and their products, |f| <= 56.25) are exact in bf16;
+    // the upstream-gradient features get a hi + lo split.
+    bf16x8 Ah[2], Al[2];
+#pragma unroll
+    for (int t2 = 0; t2 < 2; t2++) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int p = 32 * t2 + 8 * qk + j;
+            int lx2, ly2;
+            tile_pixel(w * 64 + p, lx2, ly2);
+            const float fx = (float)(tx0 + lx2) - cxT, fy = (float)(ty0 + ly2) - cyT;
+            float f = 0.f;
+            if (ql == 0) f = 1.f;
+            else if (ql == 1) f = fx;
+            else if (ql == 2) f = fy;
+            else if (ql == 3) f = fx * fx;
+            else if (ql == 4) f = fx * fy;
+            else if (ql == 5) f = fy * fy;
+            else if (ql <= 9) f = myWU[(ql - 6) * 64 + p];
+            const __bf16 h = (__bf16)f;
+            Ah[t2][j] = h;
+            Al[t2][j] = (__bf16)(f - (float)h);
+        }
+    }
+#else
     float Af[16];
 #pragma unroll
     for (int s4 = 0; s4 < 16; s4++) {
@@ -342,13 +391,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
         else if (ql <= 9) f = myWU[(ql - 6) * 64 + p];
         Af[s4] = f;
     }
+#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     auto flush_batch = [&](int nb) {
+#ifdef LGM_TIMING_SKIP_FLUSH  // timing-only diagnostic build: wrong gradients
+        return;
+#endif
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#if LGM_BWD_MFMA == 2
+        // B operand: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t), split hi + lo
+        f32x4 a2[2];
+#pragma unroll
+        for (int t2 = 0; t2 < 2; t2++) {
+            const float4 *src = reinterpret_cast<const float4 *>(myWU + ql * WU_LD + 32 * t2 + 8 * qk);
+            const float4 x0 = src[0], x1 = src[1];
+            const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            bf16x8 bh, bl;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const __bf16 h = (__bf16)xs[j];
+                bh[j] = h;
+                bl[j] = (__bf16)(xs[j] - (float)h);
+            }
+            f32x4 c = {0.f, 0.f, 0.f, 0.f};
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al[t2], bh, c, 0, 0, 0);
+            a2[t2] = c;
+        }
+        const f32x4 acc = a2[0] + a2[1];
+#else
+        // operands read up front (one LDS round trip), two accumulation chains (dependent-issue latency ~40 cyc)
+        float bq[16];
+#pragma unroll
+        for (int s4 = 0; s4 < 16; s4++) bq[s4] = myWU[ql * WU_LD + 4 * s4 + qk];
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 a2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int s4 = 0; s4 < 16; s4++)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[s4], myWU[ql * WU_LD + 4 * s4 + qk], acc, 0, 0, 0);
+            a2[s4 & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[s4], bq[s4], a2[s4 & 1], 0, 0, 0);
+        const f32x4 acc = a2[0] + a2[1];
+#endif
         // D[row = 4 qk + r][col = ql]: moments 0..5 in w columns, rows 6..9 in u columns
         if (ql < MB) {
             if (ql < nb) {
@@ -378,6 +461,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
 #endif
 
     for (int b0 = 0; b0 < nlist; b0 += TILE_PIX) {
+        SEC_T(ts0);
         __syncthreads();
         const int k = b0 + tid;  // counted from the back
         stage_entry(S, tid, k < nlist, k < nlist ? ids[nlist - 1 - k] : 0u, gbase, b, d.N, tx0, ty0, gA, gB, gD,
@@ -385,8 +469,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
 #pragma unroll
         for (int q = 0; q < NV; q++) sAcc[q * LS + tid] = 0.f;
         __syncthreads();
+        SEC_T(ts1);
+        SEC_ADD(sec_stage, ts0, ts1);
         // position nlist - 1 - (b0 + j) < wlast  <=>  j >= nlist - wlast - b0
         const int cnt = compact_wave(S, w, lane, nlist - wlast - b0);
+        SEC_T(ts2);
+        SEC_ADD(sec_compact, ts1, ts2);
         c_iter += cnt;
         // BU entries per step: G, alpha and the G-derivatives are independent of the per-pixel recurrences, so
         // they are evaluated together (ILP); the T / suffix-accumulator recurrences stay serial in list order.
@@ -427,6 +515,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
                 v[u][0] = 0.f;
                 v[u][1] = 0.f;
                 if (al[u] == 0.f) continue;
+#ifdef LGM_TIMING_SKIP_SERIAL  // timing-only diagnostic build: wrong gradients
+                v[u][0] = Gg[u];
+                v[u][1] = al[u];
+                continue;
+#endif
                 const float alpha = al[u];
                 const float4 c = cc[u];
                 Tr = Tr * inv[u];
@@ -542,11 +635,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
                 if (lane == 0) sBidx[w][nb] = (unsigned short)jj[u];
                 if (++nb == MB) {
                     c_dense++;
+                    SEC_T(tf0);
                     flush_batch(MB);
+                    SEC_T(tf1);
+                    SEC_ADD(sec_flush, tf0, tf1);
                     nb = 0;
                 }
             }
         }
+        SEC_T(ts3);
+        SEC_ADD(sec_loop, ts2, ts3);
         if (nb) {
             c_sparse++;
             flush_batch(nb);
@@ -561,7 +659,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
             const float xg = Pj.x - cxT, yg = Pj.y - cyT;
             float q[NACC];
 #pragma unroll
-            for (int qq = 0; qq < NACC; qq++) q[qq] = sAcc[qq * LS + j];
+            for (int qq = 0; qq < NV; qq++) q[qq] = sAcc[qq * LS + j];
             const float Sx = fmaf(xg, q[0], -q[1]), Sy = fmaf(yg, q[0], -q[2]);
             const float Sxx = fmaf(xg, fmaf(xg, q[0], -2.f * q[1]), q[3]);
             const float Sxy = fmaf(xg, fmaf(yg, q[0], -q[2]), fmaf(-yg, q[1], q[4]));
@@ -602,6 +700,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
         }
 #endif
         __syncthreads();
+#ifdef LGM_BWD_STAMPS
+        struct TailStamp {
+            unsigned long long t0, &acc;
+            __device__ ~TailStamp() { acc += sec_stamp() - t0; }
+        } tail_stamp{ts3, sec_tail};
+#endif
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
 #pragma unroll
@@ -614,6 +718,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
             }
         }
     }
+#ifdef LGM_BWD_STAMPS
+    if (d.counters && lane == 0) {  // shader-clock cycles per section, summed over waves: counters [2..6]
+        atomicAdd(&d.counters[2], sec_stage);
+        atomicAdd(&d.counters[3], sec_compact);
+        atomicAdd(&d.counters[4], sec_loop - sec_flush);
+        atomicAdd(&d.counters[5], sec_flush);
+        atomicAdd(&d.counters[6], sec_tail);
+    }
+    if (d.counters) return;
+#endif
     if (d.counters && tid == 0) {
         d.counters[8 + 8 * (size_t)tile + 2] = t_start;
         d.counters[8 + 8 * (size_t)tile + 3] = __builtin_amdgcn_s_memrealtime();

@@ -16,9 +16,15 @@ g = synthetic_gaussians(1, 100000, seed=1).to(dev).requires_grad_(True)
 cv, cvp, cp = orbit_cameras(6)
 d_img, _, d_alpha, bg = synthetic_upstream_grads(1, 6, 256, 256, seed=1001)
 M = 6 * 256
-NB = 6 * ((100000 + 1023) // 1024)  # k_bin workgroups (1024 Gaussians each)
-cnt = torch.zeros(8 + 8 * M + 8 * NB + 4096, dtype=torch.int64, device=dev)
+NB = 6 * ((100000 + 511) // 512)  # k_bin workgroups (512 Gaussians each)
+NI = 5 * M  # backward work-item capacity
+cnt = torch.zeros(8 + 8 * M + 8 * NB + 4 * NI, dtype=torch.int64, device=dev)
 L = _native.lib()
+for _ in range(5):  # warm up (clocks, caches, code objects) before the instrumented step
+    o = r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev), bg_color=bg.to(dev))
+    torch.autograd.backward([o["image"], o["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
+    g.grad = None
+torch.cuda.synchronize()
 L.lgm_render_debug_counters(_native.ptr(cnt))
 out = r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev), bg_color=bg.to(dev))
 torch.autograd.backward([out["image"], out["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
@@ -79,3 +85,26 @@ binres["hits_median"] = float(np.median(bt[:, 5]))
 print("k_bin phases [median us, max us]:", json.dumps(binres))
 res["k_bin_phases"] = binres
 json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)
+
+it = np.array(c[8 + 8 * M + 8 * NB: 8 + 8 * M + 8 * NB + 4 * NI], dtype=np.int64).reshape(NI, 4)
+ok = it[:, 1] > 0
+it = it[ok]
+if len(it):
+    t0 = it[:, 0].min()
+    dur = (it[:, 1] - it[:, 0]) * 0.01
+    ln = it[:, 2] & 0xFFFFF
+    lo = (it[:, 2] >> 20) & 0xFFFFF
+    tl_ = it[:, 2] >> 40
+    first = lo == 0
+    ir = {"items": int(len(it)), "span_us": round(float((it[:, 1].max() - t0) * 0.01), 2),
+          "dur_p50": round(float(np.median(dur)), 2), "dur_max": round(float(dur.max()), 2),
+          "first_seg_p50": round(float(np.median(dur[first])), 2), "first_seg_max": round(float(dur[first].max()), 2),
+          "other_seg_p50": round(float(np.median(dur[~first])), 2) if (~first).any() else None,
+          "sum_dur_us": round(float(dur.sum()), 1),
+          "last_start_us": round(float((it[:, 0].max() - t0) * 0.01), 2)}
+    order_ = np.argsort(-dur)[:8]
+    ir["slowest"] = [(int(tl_[i]), int(lo[i]), int(ln[i]), round(float(dur[i]), 2), int(it[i, 3]),
+                      round(float((it[i, 0] - t0) * 0.01), 2)) for i in order_]
+    print("bwd items:", json.dumps(ir))
+    res["bwd_items"] = ir
+    json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)

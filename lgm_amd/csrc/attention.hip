@@ -392,10 +392,463 @@ __global__ __launch_bounds__(NT) void k_attn_dkdv(int L, int H, float scale, con
     }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// forward, 16-bit inputs (v2): grid (ceil(L / (64 QS)), B*H), block 256; wavefront w owns 16 QS query rows.
+//   * S^T = K Q^T per 16-key sub-tile: the K fragment (ds_read_b128 from the row-major tile) is read once and used
+//     for all QS query sub-tiles held in registers;
+//   * P V as O^T += V^T P: the V^T operand comes straight from the row-major V tile via ds_read_b64_tr_b16 (the
+//     hardware transpose read), again shared by the QS sub-tiles;
+//   * row sums on the MFMA (ones^T P, on the same bf16/f16 P as the numerator), row max by max3 trees and the
+//     permlane16/32 swaps; masking only on the tail tile; the O rescale skipped while no row max grows;
+//   * K/V tiles double-buffered: the next tile's global loads are in flight during the current tile's MFMAs.
+template <typename T, typename V4>
+__device__ __forceinline__ V4 tr_read(const T *p) {
+    typedef __attribute__((ext_vector_type(4))) T TV4;
+    return __builtin_bit_cast(V4, *reinterpret_cast<const TV4 *>(p));
+}
+
+__device__ __forceinline__ float xmax_groups(float v) {  // max over the 4 lane groups (lanes l, l^16, l^32, l^48)
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r2[0]), __uint_as_float(r2[1]));
+}
+
+template <int DT>
+__device__ __forceinline__ typename Ty<DT>::V8 tr_frag(const typename Ty<DT>::T *tile, int ld, int k0, int d0,
+                                                      int lane) {
+    // rows k0 + 4g + (i>>2) and k0 + 16 + 4g + (i>>2), columns d0 + 4 (i&3): lane i of group g receives column
+    // d0 + i of 4 consecutive keys -> the 16x16x32 A operand of V^T with the key order of the P operand
+    using T = typename Ty<DT>::T;
+    using V8 = typename Ty<DT>::V8;
+    const int g = lane >> 4, i = lane & 15;
+    const T *p0 = tile + (k0 + 4 * g + (i >> 2)) * ld + d0 + 4 * (i & 3);
+    typedef short s4v __attribute__((__vector_size__(8)));
+    // the transposing read moves 16-bit elements regardless of type: the i16 form serves bf16 and f16
+    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v *)(p0));
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v *)(p0 + 16 * ld));
+    typedef __attribute__((ext_vector_type(8))) short s8v;
+    const s8v r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(V8, r);
+}
+
+template <int DT, int D, int QS>
+__global__ __launch_bounds__(NT) void k_attn_fwd2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+                                                  const typename Ty<DT>::T *__restrict__ k,
+                                                  const typename Ty<DT>::T *__restrict__ v, long long ld,
+                                                  typename Ty<DT>::T *__restrict__ o, float *__restrict__ lse) {
+    using T = typename Ty<DT>::T;
+    using V8 = typename Ty<DT>::V8;
+    constexpr int LDK = D + 8;                         // 16-B padded rows: conflict-free b128 row reads
+    constexpr int CH = 64 * D * 2 / 16 / NT;           // 16-B chunks per thread per tile (K or V)
+    static_assert(CH >= 1, "tile too small for the loader");
+    __shared__ __attribute__((aligned(16))) T Ks[2][64 * LDK];
+    __shared__ __attribute__((aligned(16))) T Vs[2][64 * LDK];
+    const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+    const long long base = (long long)b * L * ld + (long long)h * D;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
+    const int q0 = blockIdx.x * (64 * QS) + w * (16 * QS);
+    const float c = scale * LOG2E;
+    YFrag<DT, D> qf[QS];
+#pragma unroll
+    for (int s = 0; s < QS; s++) {
+        const int qr = q0 + 16 * s + r16;
+        load_yfrag<DT, D>(qf[s], q + base + (long long)qr * ld, qr < L, g);
+    }
+    f32x4 oacc[QS][D / 16], lacc[QS];
+    float m[QS];
+#pragma unroll
+    for (int s = 0; s < QS; s++) {
+        lacc[s] = zero4();
+        m[s] = -INFINITY;
+#pragma unroll
+        for (int dt = 0; dt < D / 16; dt++) oacc[s][dt] = zero4();
+    }
+    V8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; j++) ones[j] = (T)1.0f;
+    // tile loader (register staging)
+    uint4 kr[CH], vr[CH];
+    auto load_regs = [&](int kb) {
+#pragma unroll
+        for (int cc = 0; cc < CH; cc++) {
+            const int ci = tid + cc * NT, r = ci / (D / 8), col = (ci - r * (D / 8)) * 8;
+            const bool ok = kb + r < L;
+            const long long off = base + (long long)(kb + r) * ld + col;
+            kr[cc] = ok ? *reinterpret_cast<const uint4 *>(k + off) : make_uint4(0u, 0u, 0u, 0u);
+            vr[cc] = ok ? *reinterpret_cast<const uint4 *>(v + off) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    auto store_regs = [&](int buf) {
+#pragma unroll
+        for (int cc = 0; cc < CH; cc++) {
+            const int ci = tid + cc * NT, r = ci / (D / 8), col = (ci - r * (D / 8)) * 8;
+            *reinterpret_cast<uint4 *>(&Ks[buf][r * LDK + col]) = kr[cc];
+            *reinterpret_cast<uint4 *>(&Vs[buf][r * LDK + col]) = vr[cc];
+        }
+    };
+    load_regs(0);
+    store_regs(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kb = 0; kb < L; kb += 64) {
+        const bool more = kb + 64 < L;
+        if (more) load_regs(kb + 64);  // in flight during this tile's compute
+        const T *Kt = Ks[cur], *Vt = Vs[cur];
+        // ---- S^T sub-tiles (keys 16 sub + 4g + i, query r16 of sub-tile s)
+        f32x4 sacc[QS][4];
+#pragma unroll
+        for (int sub = 0; sub < 4; sub++) {
+            V8 kf[D / 32];
+#pragma unroll
+            for (int cc = 0; cc < D / 32; cc++)
+                kf[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+#pragma unroll
+            for (int s = 0; s < QS; s++) {
+                f32x4 a = zero4();
+#pragma unroll
+                for (int cc = 0; cc < D / 32; cc++) a = mfma32<DT>(kf[cc], qf[s].v[cc], a);
+                sacc[s][sub] = a;
+            }
+        }
+        if (kb + 64 > L) {  // tail tile: keys >= L
+#pragma unroll
+            for (int sub = 0; sub < 4; sub++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (kb + 16 * sub + 4 * g + i >= L)
+#pragma unroll
+                        for (int s = 0; s < QS; s++) sacc[s][sub][i] = -INFINITY;
+        }
+        // ---- online softmax per query sub-tile; P as the B operand (key order of tr_frag)
+        V8 pb[QS][2];
+#pragma unroll
+        for (int s = 0; s < QS; s++) {
+            float mx = fmaxf(fmaxf(sacc[s][0][0], sacc[s][0][1]), fmaxf(sacc[s][0][2], sacc[s][0][3]));
+#pragma unroll
+            for (int sub = 1; sub < 4; sub++)
+                mx = fmaxf(fmaxf(mx, sacc[s][sub][0]), fmaxf(fmaxf(sacc[s][sub][1], sacc[s][sub][2]), sacc[s][sub][3]));
+            mx = xmax_groups(mx);
+            if (__ballot(mx > m[s])) {  // some row max grew: rescale (exactly, no threshold)
+                const float mn = fmaxf(m[s], mx);
+                const float alpha = __builtin_amdgcn_exp2f((m[s] - mn) * c);  // 0 on the first tile
+#pragma unroll
+                for (int dt = 0; dt < D / 16; dt++) oacc[s][dt] *= alpha;
+                lacc[s] *= alpha;
+                m[s] = mn;
+            }
+            const float nm = -m[s] * c;
+#pragma unroll
+            for (int t = 0; t < 2; t++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    pb[s][t][i] = (T)__builtin_amdgcn_exp2f(fmaf(sacc[s][2 * t][i], c, nm));
+                    pb[s][t][4 + i] = (T)__builtin_amdgcn_exp2f(fmaf(sacc[s][2 * t + 1][i], c, nm));
+                }
+#pragma unroll
+            for (int t = 0; t < 2; t++) lacc[s] = mfma32<DT>(ones, pb[s][t], lacc[s]);
+        }
+        // ---- O^T += V^T P
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int dt = 0; dt < D / 16; dt++) {
+                const V8 vf = tr_frag<DT>(Vt, LDK, 32 * t, 16 * dt, lane);
+#pragma unroll
+                for (int s = 0; s < QS; s++) oacc[s][dt] = mfma32<DT>(vf, pb[s][t], oacc[s][dt]);
+            }
+        if (more) store_regs(cur ^ 1);  // buffer cur^1 was last read before the previous barrier
+        __syncthreads();
+        cur ^= 1;
+    }
+#pragma unroll
+    for (int s = 0; s < QS; s++) {
+        const int qr = q0 + 16 * s + r16;
+        if (qr < L) {
+            const float l = lacc[s][0];
+            const float inv = 1.f / l;
+            T *orow = o + ((long long)b * L + qr) * ((long long)H * D) + (long long)h * D;
+#pragma unroll
+            for (int dt = 0; dt < D / 16; dt++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) orow[16 * dt + 4 * g + i] = from_f<T>(oacc[s][dt][i] * inv);
+            if (g == 0) lse[(long long)bh * L + qr] = (m[s] * c + log2f(l)) * LN2;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// backward, 16-bit inputs (v2). Both kernels read their tiles row-major from LDS only: the row reads feed the
+// S / dP products, the transposed operands (Q^T, dO^T, K^T) come from the same images via ds_read_b64_tr_b16.
+// Tiles are double-buffered through registers like the forward.
+template <typename T, int D>
+struct TileLoader {  // one 64-row tile of up to two [tokens][ld] tensors, CH 16-B chunks per thread each
+    static constexpr int CH = 64 * D * 2 / 16 / NT;
+    uint4 a[CH], b[CH];
+    __device__ __forceinline__ void load(const T *pa, long long lda, const T *pb, long long ldb, int r0, int L) {
+#pragma unroll
+        for (int cc = 0; cc < CH; cc++) {
+            const int ci = threadIdx.x + cc * NT, r = ci / (D / 8), col = (ci - r * (D / 8)) * 8;
+            const bool ok = r0 + r < L;
+            a[cc] = ok ? *reinterpret_cast<const uint4 *>(pa + (long long)(r0 + r) * lda + col) : make_uint4(0u, 0u, 0u, 0u);
+            b[cc] = ok ? *reinterpret_cast<const uint4 *>(pb + (long long)(r0 + r) * ldb + col) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    __device__ __forceinline__ void store(T *ta, T *tb, int ldt) {
+#pragma unroll
+        for (int cc = 0; cc < CH; cc++) {
+            const int ci = threadIdx.x + cc * NT, r = ci / (D / 8), col = (ci - r * (D / 8)) * 8;
+            *reinterpret_cast<uint4 *>(ta + r * ldt + col) = a[cc];
+            *reinterpret_cast<uint4 *>(tb + r * ldt + col) = b[cc];
+        }
+    }
+};
+
+// dK, dV: grid (ceil(L / (64 KS)), B*H); wavefront w owns keys k0 + 16 s + (lane & 15), s < KS.
+template <int DT, int D, int KS>
+__global__ __launch_bounds__(NT) void k_attn_dkdv2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+                                                   const typename Ty<DT>::T *__restrict__ k,
+                                                   const typename Ty<DT>::T *__restrict__ v, long long ld,
+                                                   const typename Ty<DT>::T *__restrict__ dout,
+                                                   const float *__restrict__ lse, const float *__restrict__ delta,
+                                                   typename Ty<DT>::T *__restrict__ dk,
+                                                   typename Ty<DT>::T *__restrict__ dv, long long ldd) {
+    using T = typename Ty<DT>::T;
+    using V8 = typename Ty<DT>::V8;
+    constexpr int LDK = D + 8;
+    __shared__ __attribute__((aligned(16))) T Qs[2][64 * LDK];
+    __shared__ __attribute__((aligned(16))) T Os[2][64 * LDK];
+    __shared__ float sl[2][64], sd[2][64];
+    const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+    const long long base = (long long)b * L * ld + (long long)h * D;
+    const long long obase = (long long)b * L * H * D + (long long)h * D;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
+    const int k0 = blockIdx.x * (64 * KS) + w * (16 * KS);
+    const float c = scale * LOG2E;
+    YFrag<DT, D> kf[KS], vf[KS];
+#pragma unroll
+    for (int s = 0; s < KS; s++) {
+        const int kr = k0 + 16 * s + r16;
+        load_yfrag<DT, D>(kf[s], k + base + (long long)kr * ld, kr < L, g);
+        load_yfrag<DT, D>(vf[s], v + base + (long long)kr * ld, kr < L, g);
+    }
+    f32x4 dka[KS][D / 16], dva[KS][D / 16];
+#pragma unroll
+    for (int s = 0; s < KS; s++)
+#pragma unroll
+        for (int dt = 0; dt < D / 16; dt++) { dka[s][dt] = zero4(); dva[s][dt] = zero4(); }
+    TileLoader<T, D> ld_;
+    float pl = 0.f, pd = 0.f;
+    auto load_rows2 = [&](int qb) {
+        ld_.load(q + base, ld, dout + obase, (long long)H * D, qb, L);
+        if (tid < 64) {
+            const bool qv = qb + tid < L;
+            pl = qv ? lse[(long long)bh * L + qb + tid] * LOG2E : INFINITY;  // invalid rows: P = 0
+            pd = qv ? delta[(long long)bh * L + qb + tid] : 0.f;
+        }
+    };
+    auto store_rows2 = [&](int buf) {
+        ld_.store(Qs[buf], Os[buf], LDK);
+        if (tid < 64) { sl[buf][tid] = pl; sd[buf][tid] = pd; }
+    };
+    load_rows2(0);
+    store_rows2(0);
+    __syncthreads();
+    int cur = 0;
+    for (int qb = 0; qb < L; qb += 64) {
+        const bool more = qb + 64 < L;
+        if (more) load_rows2(qb + 64);
+        const T *Qt = Qs[cur], *Ot = Os[cur];
+        f32x4 sacc[KS][4], dpa[KS][4];
+#pragma unroll
+        for (int sub = 0; sub < 4; sub++) {
+            V8 qr[D / 32], orr[D / 32];
+#pragma unroll
+            for (int cc = 0; cc < D / 32; cc++) {
+                qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+            }
+#pragma unroll
+            for (int s = 0; s < KS; s++) {
+                f32x4 a = zero4(), dp = zero4();
+#pragma unroll
+                for (int cc = 0; cc < D / 32; cc++) {
+                    a = mfma32<DT>(qr[cc], kf[s].v[cc], a);     // S[q = 16 sub + 4g + i][key]
+                    dp = mfma32<DT>(orr[cc], vf[s].v[cc], dp);  // dP[q][key]
+                }
+                sacc[s][sub] = a;
+                dpa[s][sub] = dp;
+            }
+        }
+        V8 pb[KS][2], db[KS][2];
+#pragma unroll
+        for (int sub = 0; sub < 4; sub++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int qi = 16 * sub + 4 * g + i;
+                const float l2 = sl[cur][qi], dl = sd[cur][qi];
+#pragma unroll
+                for (int s = 0; s < KS; s++) {
+                    const float p = __builtin_amdgcn_exp2f(fmaf(sacc[s][sub][i], c, -l2));
+                    const float ds = p * (dpa[s][sub][i] - dl);
+                    pb[s][sub >> 1][4 * (sub & 1) + i] = (T)p;
+                    db[s][sub >> 1][4 * (sub & 1) + i] = (T)ds;
+                }
+            }
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int dt = 0; dt < D / 16; dt++) {
+                const V8 oT = tr_frag<DT>(Ot, LDK, 32 * t, 16 * dt, lane);  // dO^T
+                const V8 qT = tr_frag<DT>(Qt, LDK, 32 * t, 16 * dt, lane);  // Q^T
+#pragma unroll
+                for (int s = 0; s < KS; s++) {
+                    dva[s][dt] = mfma32<DT>(oT, pb[s][t], dva[s][dt]);
+                    dka[s][dt] = mfma32<DT>(qT, db[s][t], dka[s][dt]);
+                }
+            }
+        if (more) store_rows2(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+#pragma unroll
+    for (int s = 0; s < KS; s++) {
+        const int key = k0 + 16 * s + r16;
+        if (key < L) {
+            T *krow = dk + (long long)b * L * ldd + (long long)key * ldd + (long long)h * D;
+            T *vrow = dv + (long long)b * L * ldd + (long long)key * ldd + (long long)h * D;
+#pragma unroll
+            for (int dt = 0; dt < D / 16; dt++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    krow[16 * dt + 4 * g + i] = from_f<T>(dka[s][dt][i] * scale);
+                    vrow[16 * dt + 4 * g + i] = from_f<T>(dva[s][dt][i]);
+                }
+        }
+    }
+}
+
+// dQ: grid (ceil(L / (64 QS)), B*H); wavefront w owns query rows q0 + 16 s + (lane & 15), s < QS.
+template <int DT, int D, int QS>
+__global__ __launch_bounds__(NT) void k_attn_dq2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+                                                 const typename Ty<DT>::T *__restrict__ k,
+                                                 const typename Ty<DT>::T *__restrict__ v, long long ld,
+                                                 const typename Ty<DT>::T *__restrict__ dout,
+                                                 const float *__restrict__ lse, const float *__restrict__ delta,
+                                                 typename Ty<DT>::T *__restrict__ dq, long long ldd) {
+    using T = typename Ty<DT>::T;
+    using V8 = typename Ty<DT>::V8;
+    constexpr int LDK = D + 8;
+    __shared__ __attribute__((aligned(16))) T Ks[2][64 * LDK];
+    __shared__ __attribute__((aligned(16))) T Vs[2][64 * LDK];
+    const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+    const long long base = (long long)b * L * ld + (long long)h * D;
+    const long long obase = (long long)b * L * H * D + (long long)h * D;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
+    const int q0 = blockIdx.x * (64 * QS) + w * (16 * QS);
+    const float c = scale * LOG2E;
+    YFrag<DT, D> qf[QS], of[QS];
+    float l2[QS], dl[QS];
+#pragma unroll
+    for (int s = 0; s < QS; s++) {
+        const int qr = q0 + 16 * s + r16;
+        const bool qv = qr < L;
+        load_yfrag<DT, D>(qf[s], q + base + (long long)qr * ld, qv, g);
+        load_yfrag<DT, D>(of[s], dout + obase + (long long)qr * H * D, qv, g);
+        l2[s] = qv ? lse[(long long)bh * L + qr] * LOG2E : INFINITY;
+        dl[s] = qv ? delta[(long long)bh * L + qr] : 0.f;
+    }
+    f32x4 dqa[QS][D / 16];
+#pragma unroll
+    for (int s = 0; s < QS; s++)
+#pragma unroll
+        for (int dt = 0; dt < D / 16; dt++) dqa[s][dt] = zero4();
+    TileLoader<T, D> ld_;
+    ld_.load(k + base, ld, v + base, ld, 0, L);
+    ld_.store(Ks[0], Vs[0], LDK);
+    __syncthreads();
+    int cur = 0;
+    for (int kb = 0; kb < L; kb += 64) {
+        const bool more = kb + 64 < L;
+        if (more) ld_.load(k + base, ld, v + base, ld, kb + 64, L);
+        const T *Kt = Ks[cur], *Vt = Vs[cur];
+        f32x4 sacc[QS][4], dpa[QS][4];
+#pragma unroll
+        for (int sub = 0; sub < 4; sub++) {
+            V8 kr[D / 32], vr[D / 32];
+#pragma unroll
+            for (int cc = 0; cc < D / 32; cc++) {
+                kr[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                vr[cc] = *reinterpret_cast<const V8 *>(Vt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+            }
+#pragma unroll
+            for (int s = 0; s < QS; s++) {
+                f32x4 a = zero4(), dp = zero4();
+#pragma unroll
+                for (int cc = 0; cc < D / 32; cc++) {
+                    a = mfma32<DT>(kr[cc], qf[s].v[cc], a);    // S^T[key = 16 sub + 4g + i][q]
+                    dp = mfma32<DT>(vr[cc], of[s].v[cc], dp);  // dP^T[key][q]
+                }
+                sacc[s][sub] = a;
+                dpa[s][sub] = dp;
+            }
+        }
+        const bool tail = kb + 64 > L;
+        V8 db[QS][2];
+#pragma unroll
+        for (int sub = 0; sub < 4; sub++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const bool kv = !tail || kb + 16 * sub + 4 * g + i < L;
+#pragma unroll
+                for (int s = 0; s < QS; s++) {
+                    const float p = kv ? __builtin_amdgcn_exp2f(fmaf(sacc[s][sub][i], c, -l2[s])) : 0.f;
+                    db[s][sub >> 1][4 * (sub & 1) + i] = (T)(p * (dpa[s][sub][i] - dl[s]));
+                }
+            }
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int dt = 0; dt < D / 16; dt++) {
+                const V8 kT = tr_frag<DT>(Kt, LDK, 32 * t, 16 * dt, lane);  // K^T
+#pragma unroll
+                for (int s = 0; s < QS; s++) dqa[s][dt] = mfma32<DT>(kT, db[s][t], dqa[s][dt]);
+            }
+        if (more) ld_.store(Ks[cur ^ 1], Vs[cur ^ 1], LDK);
+        __syncthreads();
+        cur ^= 1;
+    }
+#pragma unroll
+    for (int s = 0; s < QS; s++) {
+        const int qr = q0 + 16 * s + r16;
+        if (qr < L) {
+            T *row = dq + (long long)b * L * ldd + (long long)qr * ldd + (long long)h * D;
+#pragma unroll
+            for (int dt = 0; dt < D / 16; dt++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) row[16 * dt + 4 * g + i] = from_f<T>(dqa[s][dt][i] * scale);
+        }
+    }
+}
+
 template <int DT, int D>
 int fwd_impl(int B, int L, int H, float scale, const void *q, const void *k, const void *v, long long ld, void *o,
              float *lse, hipStream_t st) {
     using T = typename Ty<DT>::T;
+    if constexpr (DT != LGM_ATTN_F32) {
+        // two query sub-tiles per wavefront when the grid stays large enough to fill the chip
+        constexpr int QS2 = D <= 64 ? 2 : 1;
+        if (QS2 == 2 && (long long)((L + 127) / 128) * B * H >= 512) {
+            dim3 grid((L + 127) / 128, B * H);
+            LGM_LAUNCH("k_attn_fwd", st, (k_attn_fwd2<DT, D, QS2><<<grid, NT, 0, st>>>(
+                                              L, H, scale, (const T *)q, (const T *)k, (const T *)v, ld, (T *)o, lse)));
+        } else {
+            dim3 grid((L + 63) / 64, B * H);
+            LGM_LAUNCH("k_attn_fwd", st, (k_attn_fwd2<DT, D, 1><<<grid, NT, 0, st>>>(
+                                              L, H, scale, (const T *)q, (const T *)k, (const T *)v, ld, (T *)o, lse)));
+        }
+        return LGM_OK;
+    }
     dim3 grid((L + BQ - 1) / BQ, B * H);
     LGM_LAUNCH("k_attn_fwd", st, (k_attn_fwd<DT, D><<<grid, NT, 0, st>>>(L, H, scale, (const T *)q, (const T *)k,
                                                                        (const T *)v, ld, (T *)o, lse)));
@@ -410,6 +863,23 @@ int bwd_impl(int B, int L, int H, float scale, const void *q, const void *k, con
     const long long rows = (long long)B * L * H;
     LGM_LAUNCH("k_attn_delta", st, (k_attn_delta<DT, D><<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(
                                        B, L, H, (const T *)o, (const T *)dout, delta)));
+    if constexpr (DT != LGM_ATTN_F32) {
+        constexpr int S2 = D <= 32 ? 2 : 1;  // two 16-row sub-tiles per wavefront where registers allow
+        const bool two = S2 == 2 && (long long)((L + 127) / 128) * B * H >= 512;
+        dim3 g2((L + (two ? 127 : 63)) / (two ? 128 : 64), B * H);
+        if (two) {
+            LGM_LAUNCH("k_attn_dq", st, (k_attn_dq2<DT, D, S2><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
+                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd)));
+            LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, S2><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
+                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dk, (T *)dv, ldd)));
+        } else {
+            LGM_LAUNCH("k_attn_dq", st, (k_attn_dq2<DT, D, 1><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
+                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd)));
+            LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, 1><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
+                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dk, (T *)dv, ldd)));
+        }
+        return LGM_OK;
+    }
     dim3 grid((L + 63) / 64, B * H);
     LGM_LAUNCH("k_attn_dq", st, (k_attn_dq<DT, D><<<grid, NT, 0, st>>>(L, H, scale, (const T *)q, (const T *)k,
                                                                      (const T *)v, ld, (const T *)dout, lse, delta,

@@ -119,7 +119,7 @@ def test_module_bf16_autocast(cuda, path):
 
 SHAPES = [  # B, L, H, D -- LGM levels (4 views x 8^2 / 16^2 / 32^2 tokens, D = 64 / 64 / 32) and ragged edges
     (1, 256, 16, 64), (2, 1024, 16, 64), (1, 4096, 16, 32), (1, 1, 2, 32), (3, 65, 2, 64), (2, 100, 3, 128),
-    (1, 17, 1, 32), (2, 600, 4, 32),
+    (1, 17, 1, 32), (2, 600, 4, 32), (2, 4100, 16, 32),  # the last one: two query sub-tiles per wave + a tail
 ]
 
 

@@ -23,6 +23,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 N_GAUSS, VIEWS, RES = 100_000, 6, 256
 
 
@@ -38,6 +39,19 @@ def kernel_bytes(N, V, K, P):
         "k_render_bwd": 84 * K + 28 * P * V,
         "k_preproc_bwd": 112 * N * V,
     }
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC profile of this workload (rocprofv3 FETCH_SIZE x 2 +
+    WRITE_SIZE, gfx950-corrected, scripts/gpu_pmc.sh -> scripts/pmc_summary.py --json), or null."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(path))
+        rec = d[kernel]
+        return {"traffic": int(rec["hbm_read_bytes"] + rec["hbm_write_bytes"]),
+                "traffic_source": f"profiles/pmc_latest.json (PMC passes at commit {d['_meta'].get('commit', '?')})"}
+    except (OSError, KeyError, ValueError):
+        return {"traffic": None}
 
 
 def cpu_baseline(g, cv, cvp, tan, bg, d_img, d_alpha, seconds):
@@ -60,6 +74,63 @@ def cpu_baseline(g, cv, cvp, tan, bg, d_img, d_alpha, seconds):
                       f"{reps} repetitions in {el:.1f} s, OpenMP over views"}
 
 
+def attention_bench(dev, steps: int = 10):
+    """Secondary object: LGM's heaviest MVAttention level (core/unet.py:35-49 at C=512, 32x32, 4 views -> L = 4096
+    tokens, 16 heads, D = 32; 8 objects per GPU as in the 'big' training batch), bf16 fwd+bwd through the HIP
+    kernels (lgm_amd/attention.py), with torch's SDPA on the same tensors as a comparator. FLOPs 14 B H L^2 D."""
+    import torch
+    import torch.nn.functional as F
+
+    from lgm_amd import _native
+    from lgm_amd.attention import packed_attention
+    B, L, H, D = 8, 4096, 16, 32
+    g = torch.Generator(device="cpu").manual_seed(7)
+    qkv = torch.randn((B, L, 3, H, D), generator=g).to(dev, torch.bfloat16)
+    d_o = torch.randn((B, L, H, D), generator=g).to(dev, torch.bfloat16)
+    x = qkv.clone().requires_grad_(True)
+
+    def step():
+        x.grad = None
+        packed_attention(x).backward(d_o)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for _ in range(steps):
+            fn()
+        en.record()
+        torch.cuda.synchronize()
+        return st.elapsed_time(en) / steps
+
+    prof = _native.KernelProfiler()
+    with prof:
+        ms = timed(step)
+    kern = prof.summary()
+    prof.close()
+    qs, ks, vs = (qkv[:, :, i].transpose(1, 2).detach().clone().requires_grad_(True) for i in range(3))
+    dos = d_o.transpose(1, 2)
+
+    def sdpa():
+        for t in (qs, ks, vs):
+            t.grad = None
+        F.scaled_dot_product_attention(qs, ks, vs).backward(dos)
+
+    try:
+        ms_sdpa = timed(sdpa)
+    except RuntimeError:
+        ms_sdpa = None
+    flops = 14.0 * B * H * L * L * D
+    tf = flops / ms / 1e9
+    return {"workload": "MVAttention C=512 32x32 x 4 views (L=4096, 16 heads, D=32), 8 objects, fwd+bwd",
+            "dtype": "bf16", "ms_per_step": round(ms, 4), "tflops": round(tf, 1),
+            "roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / PEAK_BF16_TFLOPS, 4)},
+            "kernels": {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in kern.items()},
+            "torch_sdpa_tflops": round(flops / ms_sdpa / 1e9, 1) if ms_sdpa else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,6 +138,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-attention", action="store_true", help="skip the secondary attention measurement")
     args = ap.parse_args()
 
     import torch
@@ -135,12 +207,14 @@ def main():
                    "gaussians": N_GAUSS, "views": VIEWS, "H": RES, "W": RES, "scenes_per_gpu": 1,
                    "pairs_K_reference": K, "pairs_binned": K_binned, "parallelism": f"scene-sharded x{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS,
-                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                     "bytes_per_launch": kb.get(dom, 0)},
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "bytes_per_launch": kb.get(dom, 0),
+                     **pmc_traffic(dom)},
         "step_roofline": {"bytes": step_bytes, "achieved_GBs": round(step_bytes / (ms_step / 1e3) / 1e9, 2),
                           "frac": round(step_bytes / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4)},
         "kernels": per_kernel,
     }
+    if not args.no_attention:
+        result["attention"] = attention_bench(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(g_cpu, cv[None], cvp[None], tan, bg, d_img, d_alpha,
                                               args.cpu_seconds)

@@ -31,3 +31,28 @@ for name, cs in agg.items():
         print(f"   HBM read (2 x FETCH_SIZE, gfx950 correction) MB {2 * m['FETCH_SIZE'] / 1e3:.2f}")
     if "WRITE_SIZE" in m:
         print(f"   HBM write MB {m['WRITE_SIZE'] / 1e3:.2f}")
+
+if "--json" in sys.argv:  # per-dispatch HBM bytes for bench.py's roofline.traffic (MI355X_MICROARCH.md §HBM)
+    import json
+    import subprocess
+    out = {}
+    for name, cs in agg.items():
+        m = {cn: sum(v) / len(v) for cn, v in cs.items()}
+        rec = {}
+        if "FETCH_SIZE" in m:
+            rec["hbm_read_bytes"] = 2 * m["FETCH_SIZE"] * 1024  # KiB, x2: gfx950 tallies 128-B reads at 64 B
+        if "WRITE_SIZE" in m:
+            rec["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"):
+            if k in m:
+                rec[k] = m[k]
+        out[name.split("<")[0]] = rec
+    try:
+        rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+    except OSError:
+        rev = ""
+    out["_meta"] = {"source": root, "commit": rev,
+                    "command": "rocprofv3 --kernel-trace --pmc <pass> -- python bench.py --steps 3 --warmup 2"}
+    path = sys.argv[sys.argv.index("--json") + 1]
+    json.dump(out, open(path, "w"), indent=1)
+    print("wrote", path)

@@ -28,8 +28,9 @@ for it in range(6):
     torch.cuda.synchronize()
     L.lgm_render_debug_counters(None)
     g.grad = None
-c = cnt[:8].tolist()
+c = cnt[:10].tolist()
 names = ["stage", "compact", "entries", "flush", "tail"]
 tot = sum(c[2:7])
 res = {n: {"Gcyc": round(v / 1e9, 3), "share": round(v / max(tot, 1), 3)} for n, v in zip(names, c[2:7])}
+res["quadrant_imbalance_max_over_mean"] = round(c[9] / max(c[8], 1), 3)
 print(json.dumps(res))

@@ -62,8 +62,8 @@ __device__ __forceinline__ int wave_incl_max(int v, int lane) {
 
 template <int MODE>
 __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__restrict__ gauss, const float *__restrict__ views,
-                                                     const float *__restrict__ projs, float4 *__restrict__ gA,
-                                                     float4 *__restrict__ gB, float *__restrict__ gD,
+                                                     const float *__restrict__ projs, float4 *__restrict__ gP,
+                                                     float4 *__restrict__ gQ,
                                                      uint2 *__restrict__ rects, int *__restrict__ radii_out,
                                                      int *__restrict__ tile_count, const int *__restrict__ tile_start,
                                                      unsigned long long *__restrict__ pairs, long long slot_stride,
@@ -103,18 +103,16 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         if (MODE != COUNT) {
             const size_t k = (size_t)bv * d.N + i;
             if (vis) {
-                gA[k] = make_float4(o.x, o.y, o.tau, 0.f);
-                gB[k] = make_float4(o.A, o.B, o.C, o.opacity);
-                gD[k] = o.depth;
+                gP[k] = make_float4(o.x, o.y, o.A, o.B);
+                gQ[k] = make_float4(o.C, o.opacity, o.tau, o.depth);
                 rects[k] = make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16), (unsigned)o.x1 | ((unsigned)o.y1 << 16));
                 // the backward's per-view gradient accumulators start at zero (k_preproc_bwd re-zeroes them)
                 float2 *a2 = reinterpret_cast<float2 *>(accum + k * NACC);
 #pragma unroll
                 for (int q = 0; q < NACC / 2; q++) a2[q] = make_float2(0.f, 0.f);
             } else {
-                gA[k] = make_float4(0.f, 0.f, -1.f, 0.f);
-                gB[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-                gD[k] = 0.f;
+                gP[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                gQ[k] = make_float4(0.f, 0.f, -1.f, 0.f);
                 rects[k] = make_uint2(0u, 0u);
             }
             if (radii_out) radii_out[k] = vis ? o.radius : 0;
@@ -676,8 +674,7 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
         set_error("hipMemsetAsync failed");
         return LGM_E_HIP;
     }
-    float4 *gA = (float4 *)(ws + L.gA), *gB = (float4 *)(ws + L.gB);
-    float *gD = (float *)(ws + L.gD);
+    float4 *gP = (float4 *)(ws + L.gP), *gQ = (float4 *)(ws + L.gQ);
     uint2 *rects = (uint2 *)(ws + L.rects);
     int *tcount = (int *)(ws + L.tile_count), *tstart = (int *)(ws + L.tile_start);
     unsigned long long *pairs = (unsigned long long *)(ws + L.pairs), *misc = (unsigned long long *)(ws + L.misc);
@@ -687,12 +684,12 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     if (d.N > 0) {
         if (count_only || !L.slot) {
             LGM_LAUNCH("k_bin_count", st, (k_bin<COUNT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
-                       gA, gB, gD, rects, nullptr, tcount, tstart, pairs, 0, misc, accum)));
+                       gP, gQ, rects, nullptr, tcount, tstart, pairs, 0, misc, accum)));
         }
         if (!count_only) {
             if (L.slot) {
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_SLOT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
-                           gA, gB, gD, rects, radii_out, tcount, tstart, pairs, (long long)d.N, misc, accum)));
+                           gP, gQ, rects, radii_out, tcount, tstart, pairs, (long long)d.N, misc, accum)));
             } else {
                 LGM_LAUNCH("k_scan", st, (k_scan<<<1, 1024, 0, st>>>(tcount, (int)M, tstart)));
                 if (hipMemsetAsync(ws + L.tile_count, 0, M * 4, st) != hipSuccess ||
@@ -701,7 +698,7 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                     return LGM_E_HIP;
                 }
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view,
-                           cam_view_proj, gA, gB, gD, rects, radii_out, tcount, tstart, pairs, 0, misc, accum)));
+                           cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum)));
             }
             LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M, RS_THREADS, RS_LDS, st>>>(
                                          L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs, d.counters)));

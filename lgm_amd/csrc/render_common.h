@@ -25,7 +25,7 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 //   slot mode   (pair_capacity <= 0): tile (bv, t) owns pairs[(bv*T + t) * N, +N): no counting pass, no scan.
 //   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
 struct Layout {
-    size_t gA, gB, gD, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, cmask, accum, misc, total;
+    size_t gP, gQ, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, cmask, accum, misc, total;
     long long cap;
     bool slot;
 };
@@ -37,9 +37,8 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.cap = L.slot ? (long long)(BV * T * (size_t)N) : pair_capacity;
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
-    L.gA = take(BV * N * 16);
-    L.gB = take(BV * N * 16);
-    L.gD = take(BV * N * 4);
+    L.gP = take(BV * N * 16);  // (x, y, A, B): centre and conic A, B (one 16-B row per (view, Gaussian))
+    L.gQ = take(BV * N * 16);  // (C, opacity, tau, depth)
     L.rects = take(BV * N * 8);
     L.tile_count = take(BV * T * 4);
     L.tile_start = take((BV * T + 1) * 4);

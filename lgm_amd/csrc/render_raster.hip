@@ -52,48 +52,90 @@ __device__ __forceinline__ int wave_max_i32(int v) {
 }
 
 
-// Stage entries [b0, b0 + 256) of the tile's list (fwd: front-to-back; bwd: reversed) and build the per-wave
-// compacted lists. Returns this wave's list length.
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 constexpr int WU_LD = 68;  // row stride of the per-wave [16 columns][64 pixels] gradient image (16-B aligned rows)
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 constexpr int MB = 8;      // entries per moment-MFMA batch (columns 0..7: w, 8..15: u)
 
 constexpr int SENT = TILE_PIX;  // sentinel slot: opacity 0, never contributes (pads the per-wave lists)
-struct Stage {
+// One staged 256-entry chunk, written by LDS DMA (global_load_lds: 16-B lane stride for both the 16-B and the
+// 12-B form): P from gP, Q from gQ, R.xyz from the Gaussian row's colour; R.w holds the Gaussian id (written
+// at commit). Two of these alternate: chunk c+1 streams into one while chunk c is composited from the other.
+struct StageBuf {
     float4 P[TILE_PIX + 1];  // x, y, A, B
-    float2 Q[TILE_PIX + 1];  // C, opacity
-    float4 R[TILE_PIX + 1];  // r, g, b, depth
-    unsigned id[TILE_PIX];
-    unsigned char mask[TILE_PIX];
+    float4 Q[TILE_PIX + 1];  // C, opacity, tau, depth
+    float4 R[TILE_PIX + 1];  // r, g, b, id bits
+};
+template <int NB>  // 2: double-buffered (the backward), 1: synchronous staging (the forward)
+struct StageT {
+    StageBuf buf[NB];
+    unsigned char mask[TILE_PIX];          // quadrant mask of the current chunk's entries
     unsigned short list[4][TILE_PIX + 4];  // per-wave compacted entry indices, padded with SENT to a multiple of 4
 };
+#ifndef LGM_FWD_DB
+#define LGM_FWD_DB 0  // forward staging double-buffered (1) or synchronous (0): the forward usually stops early
+#endif
+using StageFwd = StageT<LGM_FWD_DB ? 2 : 1>;
+using StageBwd = StageT<2>;
 
-__device__ __forceinline__ void stage_entry(Stage &S, int j, bool have, unsigned gid, size_t gbase, int b, int N,
-                                            int tx0, int ty0, const float4 *__restrict__ gA,
-                                            const float4 *__restrict__ gB, const float *__restrict__ gD,
-                                            const float *__restrict__ gauss) {
+// Wait for every outstanding vector-memory operation of this wave (incl. its LDS DMA). A hard s_waitcnt: the
+// compiler's waitcnt pass sees it, and does not itself track LDS written by DMA.
+__device__ __forceinline__ void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0) only
+
+// LDS DMA (global_load_lds_dwordx{3,4}: lane i's bytes land at M0 + 16 i). Issued from inline asm on purpose:
+// the compiler's waitcnt pass treats any later LDS access that may alias a pending DMA as dependent on it and
+// would wait for the prefetch right after issuing it. Hidden from the pass, the DMA only makes the pass's own
+// vmcnt waits more conservative (still correct); its completion is ordered explicitly by vm_wait_all() plus a
+// barrier. M0 is saved and restored around it (the compiler owns M0), with the M0 -> LDS-DMA wait state.
+template <int BYTES>
+__device__ __forceinline__ void lds_dma(const void *src, void *lds_row0) {
+    const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_row0);
+    unsigned saved;
+    if (BYTES == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(saved)
+                     : "s"(m), "v"(src)
+                     : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx3 %2, off\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(saved)
+                     : "s"(m), "v"(src)
+                     : "memory");
+}
+
+// Issue the LDS DMA of one entry (this lane's row of wave w's 64-row slice). Asynchronous: the rows are valid
+// after vm_wait_all() in every issuing wave followed by a barrier.
+__device__ __forceinline__ void stage_dma(StageBuf &B, int w, unsigned gid, size_t gbase, int b, int N,
+                                          const float4 *__restrict__ gP, const float4 *__restrict__ gQ,
+                                          const float *__restrict__ gauss) {
+    lds_dma<16>(gP + gbase + gid, &B.P[w * 64]);
+    lds_dma<16>(gQ + gbase + gid, &B.Q[w * 64]);
+    lds_dma<12>(gauss + ((size_t)b * N + gid) * 14 + 11, &B.R[w * 64]);
+}
+
+// Entry j of a landed chunk: its quadrant mask (the alpha >= 1/255 ellipse against the four 8x8 quadrants) and,
+// for the backward's gradient flush, its Gaussian id.
+template <class Stage>
+__device__ __forceinline__ void stage_commit(Stage &S, StageBuf &B, int j, bool have, unsigned gid, int tx0, int ty0,
+                                             bool store_id) {
     unsigned char mask = 0;
     if (have) {
-        const float4 a = gA[gbase + gid];
-        const float4 bb = gB[gbase + gid];
-        const float dep = gD[gbase + gid];
-        const float *c = gauss + ((size_t)b * N + gid) * 14 + 11;
-        S.P[j] = make_float4(a.x, a.y, bb.x, bb.y);
-        S.Q[j] = make_float2(bb.z, bb.w);
-        S.R[j] = make_float4(c[0], c[1], c[2], dep);
-        S.id[j] = gid;
-        const float iA = 1.0f / bb.x, iC = 1.0f / bb.z;
+        const float4 p = B.P[j], q = B.Q[j];
+        if (store_id) reinterpret_cast<unsigned *>(&B.R[j])[3] = gid;
+        const float iA = 1.0f / p.z, iC = 1.0f / q.x;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const float qx = (float)(tx0 + ((q & 1) << 3)), qy = (float)(ty0 + ((q >> 1) << 3));
-            if (ellipse_hits_rect(a.x, a.y, bb.x, bb.y, bb.z, iA, iC, a.z, qx, qx + 7.0f, qy, qy + 7.0f))
-                mask |= (unsigned char)(1u << q);
+        for (int k = 0; k < 4; k++) {
+            const float qx = (float)(tx0 + ((k & 1) << 3)), qy = (float)(ty0 + ((k >> 1) << 3));
+            if (ellipse_hits_rect(p.x, p.y, p.z, p.w, q.x, iA, iC, q.z, qx, qx + 7.0f, qy, qy + 7.0f))
+                mask |= (unsigned char)(1u << k);
         }
     }
     S.mask[j] = mask;
 }
 
+template <class Stage>
 __device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin = 0) {
     int cnt = 0;
     const unsigned long long lt = lanemask_lt(lane);
@@ -110,6 +152,7 @@ __device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin 
 }
 
 // Four consecutive list entries as wave-uniform (scalar) indices.
+template <class Stage>
 __device__ __forceinline__ void list4(const Stage &S, int w, int kk, int (&jj)[4]) {
     const uint2 v = *reinterpret_cast<const uint2 *>(&S.list[w][kk]);
     const unsigned lo = __builtin_amdgcn_readfirstlane(v.x), hi = __builtin_amdgcn_readfirstlane(v.y);
@@ -119,11 +162,13 @@ __device__ __forceinline__ void list4(const Stage &S, int w, int kk, int (&jj)[4
     jj[3] = hi >> 16;
 }
 
+template <class Stage>
 __device__ __forceinline__ void init_sentinel(Stage &S) {
-    if (threadIdx.x == 0) {
-        S.P[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
-        S.Q[SENT] = make_float2(0.f, 0.f);
-        S.R[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (threadIdx.x < sizeof(S.buf) / sizeof(S.buf[0])) {
+        StageBuf &B = S.buf[threadIdx.x];
+        B.P[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
+        B.Q[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
+        B.R[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 
@@ -132,13 +177,13 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
                                                     const int *__restrict__ tile_start,
                                                     const int *__restrict__ tile_count,
                                                     const unsigned long long *__restrict__ pairs,
-                                                    const float4 *__restrict__ gA, const float4 *__restrict__ gB,
-                                                    const float *__restrict__ gD, const float *__restrict__ gauss,
+                                                    const float4 *__restrict__ gP, const float4 *__restrict__ gQ,
+                                                    const float *__restrict__ gauss,
                                                     const float *__restrict__ bg, float *__restrict__ out_img,
                                                     float *__restrict__ out_depth, float *__restrict__ out_alpha,
                                                     float *__restrict__ final_T, int *__restrict__ n_contrib,
                                                     unsigned char *__restrict__ cmask) {
-    __shared__ Stage S;
+    __shared__ StageFwd S;
     const int tile = order[blockIdx.x];  // longest lists first (k_order)
     const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
     const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
@@ -160,12 +205,38 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
     int last = 0;
     constexpr int FU = 4;
     unsigned c_iter = 0, c_acc = 0, c_list = 0;  // diagnostic work counters (Dims::counters)
-    for (int b0 = 0; b0 < n; b0 += TILE_PIX) {
+#if LGM_FWD_DB
+    // staging pipeline: chunk c+1's entries stream into the other buffer by LDS DMA while chunk c is composited;
+    // the sorted ids run one chunk further ahead in a register
+    if (tid < n) stage_dma(S.buf[0], w, ids[tid], gbase, b, d.N, gP, gQ, gauss);
+    unsigned id_next = TILE_PIX + tid < n ? ids[TILE_PIX + tid] : 0u;
+    int cur = 0;
+    for (int b0 = 0; b0 < n; b0 += TILE_PIX, cur ^= 1) {
+        vm_wait_all();  // this wave's share of chunk c has landed; the barrier below publishes all four
         if (__syncthreads_count(done) == TILE_PIX) break;
         c_list += min(TILE_PIX, n - b0);
         const int k = b0 + tid;
-        stage_entry(S, tid, k < n, k < n ? ids[k] : 0u, gbase, b, d.N, tx0, ty0, gA, gB, gD, gauss);
+        StageBuf &B = S.buf[cur];
+        stage_commit(S, B, tid, k < n, 0u, tx0, ty0, false);
         __syncthreads();
+        if (k + TILE_PIX < n) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
+        id_next = k + 2 * TILE_PIX < n ? ids[k + 2 * TILE_PIX] : 0u;
+#else
+    // synchronous staging (most tiles stop within a chunk or two, so a prefetched chunk would mostly be wasted):
+    // one LDS DMA round trip per chunk, the sorted ids loaded a chunk ahead; each lane tests its own entry as soon
+    // as its row has landed, so one barrier publishes rows and masks together
+    unsigned id_cur = tid < n ? ids[tid] : 0u;
+    StageBuf &B = S.buf[0];
+    for (int b0 = 0; b0 < n; b0 += TILE_PIX) {
+        if (__syncthreads_count(done) == TILE_PIX) break;  // also: every wave is done with the previous chunk
+        c_list += min(TILE_PIX, n - b0);
+        const int k = b0 + tid;
+        if (k < n) stage_dma(B, w, id_cur, gbase, b, d.N, gP, gQ, gauss);
+        id_cur = k + TILE_PIX < n ? ids[k + TILE_PIX] : 0u;
+        vm_wait_all();
+        stage_commit(S, B, tid, k < n, 0u, tx0, ty0, false);
+        __syncthreads();
+#endif
         const int cnt = compact_wave(S, w, lane);
         // FU = 4 entries per step: their alphas are independent of the running transmittance, so they are evaluated
         // together (ILP, branch-free: list padded with the opacity-0 sentinel); only the short T / colour update
@@ -179,9 +250,10 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
             float4 cc[FU];
 #pragma unroll
             for (int u = 0; u < FU; u++) {
-                const float4 P = S.P[jj[u]];
-                const float2 Q = S.Q[jj[u]];
-                cc[u] = S.R[jj[u]];
+                const float4 P = B.P[jj[u]];
+                const float4 Q = B.Q[jj[u]];
+                const float4 R = B.R[jj[u]];
+                cc[u] = make_float4(R.x, R.y, R.z, Q.w);
                 const float dx = P.x - pfx, dy = P.y - pfy;
                 const float power = -0.5f * (P.z * dx * dx + Q.x * dy * dy) - P.w * dx * dy;
                 const float alpha = fminf(0.99f, Q.y * __builtin_amdgcn_exp2f(power * LOG2E));
@@ -206,6 +278,9 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
             }
         }
     }
+#if LGM_FWD_DB
+    vm_wait_all();  // no LDS DMA may still be in flight when the workgroup retires (early termination)
+#endif
     if (d.counters) {
         c_acc = (unsigned)__reduce_add_wave(c_acc);
         if (lane == 0) {
@@ -257,12 +332,12 @@ __device__ __forceinline__ float row_sum16(float v) {
 #define LGM_BWD_WPE 3  // minimum waves per SIMD the register allocation must allow (4: <= 128 VGPRs)
 #endif
 template <bool DEPTH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE))) void k_render_bwd(Dims d, long long slot_stride, const int *__restrict__ order,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 : LGM_BWD_WPE))) void k_render_bwd(Dims d, long long slot_stride, const int *__restrict__ order,
                                                     const int *__restrict__ tile_start,
                                                     const int *__restrict__ tile_count,
                                                     const unsigned long long *__restrict__ pairs,
-                                                    const float4 *__restrict__ gA, const float4 *__restrict__ gB,
-                                                    const float *__restrict__ gD, const float *__restrict__ gauss,
+                                                    const float4 *__restrict__ gP, const float4 *__restrict__ gQ,
+                                                    const float *__restrict__ gauss,
                                                     const float *__restrict__ bg, const float *__restrict__ final_T,
                                                     const int *__restrict__ n_contrib,
                                                     const float *__restrict__ d_img,
@@ -272,7 +347,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
                                                     float *__restrict__ accum) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
     constexpr int LS = TILE_PIX + 1;             // padded LDS row stride (no bank conflicts)
-    __shared__ Stage S;
+    __shared__ StageBwd S;
     __shared__ float sAcc[LS * NV];  // 9 rows without a depth gradient: 4 workgroups fit in the CU's LDS
     __shared__ int sMaxLast;
 #if LGM_BWD_MFMA
@@ -460,15 +535,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
     };
 #endif
 
-    for (int b0 = 0; b0 < nlist; b0 += TILE_PIX) {
+    // Staging pipeline (the list walked back to front): chunk c+1 streams into the other buffer by LDS DMA during
+    // chunk c's compositing, and is complete (vm_wait_all) before chunk c's gradient atomics are issued, so no
+    // staging load ever queues behind them; the sorted ids run one chunk further ahead in a register.
+    unsigned id_cur = tid < nlist ? ids[nlist - 1 - tid] : 0u;
+    if (tid < nlist) stage_dma(S.buf[0], w, id_cur, gbase, b, d.N, gP, gQ, gauss);
+    unsigned id_next = TILE_PIX + tid < nlist ? ids[nlist - 1 - TILE_PIX - tid] : 0u;
+    vm_wait_all();
+    int cur = 0;
+    for (int b0 = 0; b0 < nlist; b0 += TILE_PIX, cur ^= 1) {
         SEC_T(ts0);
         __syncthreads();
         const int k = b0 + tid;  // counted from the back
-        stage_entry(S, tid, k < nlist, k < nlist ? ids[nlist - 1 - k] : 0u, gbase, b, d.N, tx0, ty0, gA, gB, gD,
-                    gauss);
+        StageBuf &B = S.buf[cur];
+        stage_commit(S, B, tid, k < nlist, id_cur, tx0, ty0, true);
 #pragma unroll
         for (int q = 0; q < NV; q++) sAcc[q * LS + tid] = 0.f;
         __syncthreads();
+        if (k + TILE_PIX < nlist) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
+        id_cur = id_next;
+        id_next = k + 2 * TILE_PIX < nlist ? ids[nlist - 1 - (k + 2 * TILE_PIX)] : 0u;
         SEC_T(ts1);
         SEC_ADD(sec_stage, ts0, ts1);
         // position nlist - 1 - (b0 + j) < wlast  <=>  j >= nlist - wlast - b0
@@ -494,9 +580,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
 #pragma unroll
             for (int u = 0; u < BU; u++) {
                 const int pos = nlist - 1 - (b0 + jj[u]);  // 0-based position in the tile list
-                const float4 Pj = S.P[jj[u]];
-                const float2 Q = S.Q[jj[u]];
-                cc[u] = S.R[jj[u]];
+                const float4 Pj = B.P[jj[u]];
+                const float4 Q = B.Q[jj[u]];
+                const float4 Rj = B.R[jj[u]];
+                cc[u] = make_float4(Rj.x, Rj.y, Rj.z, Q.w);
                 const float dx = Pj.x - pfx, dy = Pj.y - pfy;
                 const float power = -0.5f * (Pj.z * dx * dx + Q.x * dy * dy) - Pj.w * dx * dy;
                 const float G = __builtin_amdgcn_exp2f(power * LOG2E);
@@ -556,9 +643,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
 #pragma unroll
                 for (int q = 0; q < NACC; q++) v[u][q] = 0.f;
                 const int pos = nlist - 1 - (b0 + jj[u]);  // 0-based position in the tile list
-                const float4 Pj = S.P[jj[u]];
-                const float2 Q = S.Q[jj[u]];
-                cc[u] = S.R[jj[u]];
+                const float4 Pj = B.P[jj[u]];
+                const float4 Q = B.Q[jj[u]];
+                const float4 Rj = B.R[jj[u]];
+                cc[u] = make_float4(Rj.x, Rj.y, Rj.z, Q.w);
                 const float dx = Pj.x - pfx, dy = Pj.y - pfy;
                 const float power = -0.5f * (Pj.z * dx * dx + Q.x * dy * dy) - Pj.w * dx * dy;
                 const float G = __builtin_amdgcn_exp2f(power * LOG2E);
@@ -654,8 +742,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
         // moments -> gradient partials, in place (one thread per staged entry)
         if (b0 + tid < nlist) {
             const int j = tid;
-            const float4 Pj = S.P[j];
-            const float2 Qj = S.Q[j];
+            const float4 Pj = B.P[j];
+            const float4 Qj = B.Q[j];
             const float xg = Pj.x - cxT, yg = Pj.y - cyT;
             float q[NACC];
 #pragma unroll
@@ -699,6 +787,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
             }
         }
 #endif
+        vm_wait_all();  // chunk c+1's DMA and ids have landed: the atomics below cannot delay them
         __syncthreads();
 #ifdef LGM_BWD_STAMPS
         struct TailStamp {
@@ -714,7 +803,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_BWD_WPE
             const int j = f / NACC, q = f - j * NACC;
             if (q < NV && b0 + j < nlist) {
                 const float a = sAcc[q * LS + j];
-                if (a != 0.f) atomicAdd(accum + (gbase + S.id[j]) * NACC + q, a);
+#ifndef LGM_TIMING_SKIP_ATOMICS  // timing-only diagnostic build: wrong gradients
+                if (a != 0.f) atomicAdd(accum + (gbase + reinterpret_cast<const unsigned *>(&B.R[j])[3]) * NACC + q, a);
+#endif
             }
         }
     }
@@ -881,8 +972,8 @@ int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, fl
     LGM_LAUNCH("k_render_fwd", st, (k_render_fwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
-                                       (const float4 *)(ws + L.gA), (const float4 *)(ws + L.gB),
-                                       (const float *)(ws + L.gD), gaussians, bg, image, depth, alpha,
+                                       (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
+                                       image, depth, alpha,
                                        (float *)(ws + L.final_T), (int *)(ws + L.n_contrib),
                                        (unsigned char *)(ws + L.cmask))));
     return LGM_OK;
@@ -895,8 +986,8 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
     LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
-                                       (const float4 *)(ws + L.gA), (const float4 *)(ws + L.gB),
-                                       (const float *)(ws + L.gD), gaussians, bg, (const float *)(ws + L.final_T),
+                                       (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
+                                       (const float *)(ws + L.final_T),
                                        (const int *)(ws + L.n_contrib), d_image, d_depth, d_alpha,
                                        (const unsigned char *)(ws + L.cmask),
                                        (float *)(ws + L.accum))));

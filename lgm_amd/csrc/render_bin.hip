@@ -275,16 +275,16 @@ __global__ __launch_bounds__(1024) void k_scan(const int *__restrict__ count, in
     if (tid == 1023) start[M] = (int)wsum[15];
 }
 
-// k_order: one workgroup; the (view, tile) work items sorted by decreasing bucket size (counting sort on
-// n / 8). The compositing kernels take their tiles in this order, so the longest lists start first and the
-// short ones fill the gaps (longest-processing-time-first scheduling).
+// LPT order: the (view, tile) work items sorted by decreasing bucket size (counting sort on n / 8). The
+// compositing kernels take their tiles in this order, so the longest lists start first and the short ones fill
+// the gaps (longest-processing-time-first scheduling). One workgroup of NT threads; hist: ORD_BK ints of LDS.
 constexpr int ORD_THREADS = 1024, ORD_BK = 2048;
-__global__ __launch_bounds__(ORD_THREADS) void k_order(int M, long long slot_stride, const int *__restrict__ tile_start,
-                                                       const int *__restrict__ tile_count, int *__restrict__ order) {
-    __shared__ int hist[ORD_BK];
-    __shared__ int s_wsum[ORD_THREADS / 64];
+template <int NT>
+__device__ __forceinline__ void order_tiles(int M, long long slot_stride, const int *__restrict__ tile_start,
+                                            const int *__restrict__ tile_count, int *__restrict__ order, int *hist,
+                                            int *s_wsum) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int q = tid; q < ORD_BK; q += ORD_THREADS) hist[q] = 0;
+    for (int q = tid; q < ORD_BK; q += NT) hist[q] = 0;
     __syncthreads();
     auto key = [&](int t) {
         long long base;
@@ -292,10 +292,10 @@ __global__ __launch_bounds__(ORD_THREADS) void k_order(int M, long long slot_str
         tile_range(t, slot_stride, tile_start, tile_count, base, n);
         return ORD_BK - 1 - min(n >> 3, ORD_BK - 1);  // descending size
     };
-    for (int t = tid; t < M; t += ORD_THREADS) atomicAdd(&hist[key(t)], 1);
+    for (int t = tid; t < M; t += NT) atomicAdd(&hist[key(t)], 1);
     __syncthreads();
-    // exclusive scan of ORD_BK counters, ORD_BK / ORD_THREADS per thread
-    constexpr int PER = ORD_BK / ORD_THREADS;
+    // exclusive scan of ORD_BK counters, ORD_BK / NT per thread
+    constexpr int PER = ORD_BK / NT;
     int loc[PER], sum = 0;
 #pragma unroll
     for (int j = 0; j < PER; j++) { loc[j] = hist[tid * PER + j]; sum += loc[j]; }
@@ -312,7 +312,16 @@ __global__ __launch_bounds__(ORD_THREADS) void k_order(int M, long long slot_str
 #pragma unroll
     for (int j = 0; j < PER; j++) { hist[tid * PER + j] = run; run += loc[j]; }
     __syncthreads();
-    for (int t = tid; t < M; t += ORD_THREADS) order[atomicAdd(&hist[key(t)], 1)] = t;
+    for (int t = tid; t < M; t += NT) order[atomicAdd(&hist[key(t)], 1)] = t;
+}
+
+// k_order: the LPT order on its own (only when there is nothing to sort: N == 0; otherwise k_sort's
+// workgroup 0 computes it alongside the tile sorts).
+__global__ __launch_bounds__(ORD_THREADS) void k_order(int M, long long slot_stride, const int *__restrict__ tile_start,
+                                                       const int *__restrict__ tile_count, int *__restrict__ order) {
+    __shared__ int hist[ORD_BK];
+    __shared__ int s_wsum[ORD_THREADS / 64];
+    order_tiles<ORD_THREADS>(M, slot_stride, tile_start, tile_count, order, hist, s_wsum);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -642,23 +651,33 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     }
 }
 
-// k_sort: grid (B*V*T), block RS_THREADS, dynamic LDS RS_LDS bytes.
-__global__ __launch_bounds__(RS_THREADS) void k_sort(long long slot_stride, const int *__restrict__ tile_start,
+// k_sort: grid (1 + B*V*T), block RS_THREADS, dynamic LDS RS_LDS bytes. Workgroup 0 computes the LPT order
+// (it reads only the final tile counts, so it runs alongside the sorts and saves a dependent launch); workgroup
+// 1 + t sorts tile t.
+__global__ __launch_bounds__(RS_THREADS) void k_sort(int M, long long slot_stride, const int *__restrict__ tile_start,
                                                      const int *__restrict__ tile_count,
-                                                     unsigned long long *__restrict__ pairs,
+                                                     unsigned long long *__restrict__ pairs, int *__restrict__ order,
                                                      unsigned long long *__restrict__ counters) {
+    if (blockIdx.x == 0) {
+        extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+        static_assert(RS_LDS >= (ORD_BK + RS_WAVES) * 4, "order_tiles reuses the sort image");
+        int *hist = reinterpret_cast<int *>(smem);
+        order_tiles<RS_THREADS>(M, slot_stride, tile_start, tile_count, order, hist, hist + ORD_BK);
+        return;
+    }
+    const int tile = blockIdx.x - 1;
     long long base;
     int n;
-    tile_range(blockIdx.x, slot_stride, tile_start, tile_count, base, n);
+    tile_range(tile, slot_stride, tile_start, tile_count, base, n);
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     if (counters && threadIdx.x == 0) {  // per-workgroup timeline + bucket size (see lgm_render_debug_counters)
-        counters[8 + 8 * (size_t)blockIdx.x + 4] = t_start;
-        counters[8 + 8 * (size_t)blockIdx.x + 6] = (unsigned long long)n;
+        counters[8 + 8 * (size_t)tile + 4] = t_start;
+        counters[8 + 8 * (size_t)tile + 6] = (unsigned long long)n;
     }
     sort_tile(base, n, pairs);
     if (counters) {
         __syncthreads();
-        if (threadIdx.x == 0) counters[8 + 8 * (size_t)blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) counters[8 + 8 * (size_t)tile + 5] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -669,8 +688,8 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                    char *ws, const Layout &L, int *radii_out, long long *stats_out, bool count_only,
                    hipStream_t st) {
     const size_t M = (size_t)d.BV * d.T;
-    if (hipMemsetAsync(ws + L.tile_count, 0, M * 4, st) != hipSuccess ||
-        hipMemsetAsync(ws + L.misc, 0, 64, st) != hipSuccess) {
+    // tile counters and the misc counters are adjacent in the layout: one memset
+    if (hipMemsetAsync(ws + L.tile_count, 0, L.misc + 64 - L.tile_count, st) != hipSuccess) {
         set_error("hipMemsetAsync failed");
         return LGM_E_HIP;
     }
@@ -692,23 +711,23 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                            gP, gQ, rects, radii_out, tcount, tstart, pairs, (long long)d.N, misc, accum)));
             } else {
                 LGM_LAUNCH("k_scan", st, (k_scan<<<1, 1024, 0, st>>>(tcount, (int)M, tstart)));
-                if (hipMemsetAsync(ws + L.tile_count, 0, M * 4, st) != hipSuccess ||
-                    hipMemsetAsync(ws + L.misc, 0, 64, st) != hipSuccess) {
+                if (hipMemsetAsync(ws + L.tile_count, 0, L.misc + 64 - L.tile_count, st) != hipSuccess) {
                     set_error("hipMemsetAsync failed");
                     return LGM_E_HIP;
                 }
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view,
                            cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum)));
             }
-            LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M, RS_THREADS, RS_LDS, st>>>(
-                                         L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs, d.counters)));
+            LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M + 1, RS_THREADS, RS_LDS, st>>>(
+                                         (int)M, L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs,
+                                         (int *)(ws + L.order), d.counters)));
         }
     }
     if (d.N == 0 && !L.slot && hipMemsetAsync(ws + L.tile_start, 0, (M + 1) * 4, st) != hipSuccess) {
         set_error("hipMemsetAsync failed");  // packed mode with no Gaussians: every tile range is empty
         return LGM_E_HIP;
     }
-    if (!count_only) {  // also for N == 0: the compositing kernels index their tiles through it
+    if (!count_only && d.N == 0) {  // the compositing kernels index their tiles through it (else: k_sort's WG 0)
         LGM_LAUNCH("k_order", st, (k_order<<<1, ORD_THREADS, 0, st>>>((int)M, L.slot ? (long long)d.N : -1LL,
                                                                      tstart, tcount, (int *)(ws + L.order))));
     }

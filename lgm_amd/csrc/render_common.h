@@ -41,6 +41,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.gQ = take(BV * N * 16);  // (C, opacity, tau, depth)
     L.rects = take(BV * N * 8);
     L.tile_count = take(BV * T * 4);
+    L.misc = take(64);  // right after tile_count: the binning clears both with one memset
     L.tile_start = take((BV * T + 1) * 4);
     L.order = take(BV * T * 4);
     L.pairs = take((size_t)L.cap * 8);
@@ -48,7 +49,6 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.n_contrib = take(BV * P * 4);
     L.cmask = take(BV * P);
     L.accum = take(BV * N * NACC * 4);
-    L.misc = take(64);
     L.total = o;
     return L;
 }

@@ -10,7 +10,10 @@
 #include "render_common.h"
 
 #ifndef LGM_BWD_BU
-#define LGM_BWD_BU 2  // backward entries evaluated per step (ILP vs registers)
+#define LGM_BWD_BU 4  // backward entries evaluated per step (ILP vs registers): 1, 2 or 4
+#endif
+#ifndef LGM_FWD_FU
+#define LGM_FWD_FU 4  // forward entries evaluated per step: 4 or 8
 #endif
 #ifndef LGM_BWD_MFMA
 // per-entry gradient sums as pixel moments on the MFMA: 1 = exact-f32 16x16x4, 2 = split-bf16 16x16x32 (features
@@ -66,17 +69,18 @@ struct StageBuf {
     float4 Q[TILE_PIX + 1];  // C, opacity, tau, depth
     float4 R[TILE_PIX + 1];  // r, g, b, id bits
 };
-template <int NB>  // 2: double-buffered (the backward), 1: synchronous staging (the forward)
-struct StageT {
+template <int NB, int PAD>  // NB 2: double-buffered (the backward), 1: synchronous staging (the forward)
+struct StageT {                // PAD: list padding = entries evaluated per step (a multiple of 4)
     StageBuf buf[NB];
     unsigned char mask[TILE_PIX];          // quadrant mask of the current chunk's entries
-    unsigned short list[4][TILE_PIX + 4];  // per-wave compacted entry indices, padded with SENT to a multiple of 4
+    unsigned short list[4][TILE_PIX + PAD];  // per-wave compacted entry indices, padded with SENT to a multiple of PAD
 };
 #ifndef LGM_FWD_DB
 #define LGM_FWD_DB 0  // forward staging double-buffered (1) or synchronous (0): the forward usually stops early
 #endif
-using StageFwd = StageT<LGM_FWD_DB ? 2 : 1>;
-using StageBwd = StageT<2>;
+using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
+// the backward sits 3 workgroups per CU only just: its LDS must stay <= 53,744 B (measured: 53,776 B ran at 2)
+using StageBwd = StageT<2, 4>;
 
 // Wait for every outstanding vector-memory operation of this wave (incl. its LDS DMA). A hard s_waitcnt: the
 // compiler's waitcnt pass sees it, and does not itself track LDS written by DMA.
@@ -137,6 +141,7 @@ __device__ __forceinline__ void stage_commit(Stage &S, StageBuf &B, int j, bool 
 
 template <class Stage>
 __device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin = 0) {
+    constexpr int PAD = (int)(sizeof(S.list[0]) / sizeof(S.list[0][0])) - TILE_PIX;
     int cnt = 0;
     const unsigned long long lt = lanemask_lt(lane);
 #pragma unroll
@@ -147,19 +152,23 @@ __device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin 
         if (bit) S.list[w][cnt + __popcll(bal & lt)] = (unsigned short)j;
         cnt += __popcll(bal);
     }
-    if (lane < 4) S.list[w][cnt + lane] = (unsigned short)SENT;  // pad to the next multiple of 4
+    if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)SENT;  // pad to the next multiple of PAD
     return cnt;
 }
 
-// Four consecutive list entries as wave-uniform (scalar) indices.
-template <class Stage>
-__device__ __forceinline__ void list4(const Stage &S, int w, int kk, int (&jj)[4]) {
-    const uint2 v = *reinterpret_cast<const uint2 *>(&S.list[w][kk]);
-    const unsigned lo = __builtin_amdgcn_readfirstlane(v.x), hi = __builtin_amdgcn_readfirstlane(v.y);
-    jj[0] = lo & 0xffffu;
-    jj[1] = lo >> 16;
-    jj[2] = hi & 0xffffu;
-    jj[3] = hi >> 16;
+// U (a multiple of 4) consecutive list entries from kk (a multiple of 4) as wave-uniform (scalar) indices.
+template <int U, class Stage>
+__device__ __forceinline__ void list_n(const Stage &S, int w, int kk, int (&jj)[U]) {
+    static_assert(U % 4 == 0, "list reads are 8-B words");
+#pragma unroll
+    for (int h = 0; h < U / 4; h++) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(&S.list[w][kk + 4 * h]);
+        const unsigned lo = __builtin_amdgcn_readfirstlane(v.x), hi = __builtin_amdgcn_readfirstlane(v.y);
+        jj[4 * h + 0] = lo & 0xffffu;
+        jj[4 * h + 1] = lo >> 16;
+        jj[4 * h + 2] = hi & 0xffffu;
+        jj[4 * h + 3] = hi >> 16;
+    }
 }
 
 template <class Stage>
@@ -203,7 +212,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
     bool done = !inside;
     float Tr = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     int last = 0;
-    constexpr int FU = 4;
+    constexpr int FU = LGM_FWD_FU;
     unsigned c_iter = 0, c_acc = 0, c_list = 0;  // diagnostic work counters (Dims::counters)
 #if LGM_FWD_DB
     // staging pipeline: chunk c+1's entries stream into the other buffer by LDS DMA while chunk c is composited;
@@ -245,7 +254,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
             if (__ballot(!done) == 0ull) break;
             c_iter += min(FU, cnt - kk);
             int jj[FU];
-            list4(S, w, kk, jj);
+            list_n(S, w, kk, jj);
             float al[FU];
             float4 cc[FU];
 #pragma unroll
@@ -348,10 +357,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
     constexpr int LS = TILE_PIX + 1;             // padded LDS row stride (no bank conflicts)
     __shared__ StageBwd S;
-    __shared__ float sAcc[LS * NV];  // 9 rows without a depth gradient: 4 workgroups fit in the CU's LDS
+    __shared__ __attribute__((aligned(16))) float sAcc[LS * NV];  // 9 rows without a depth gradient
     __shared__ int sMaxLast;
 #if LGM_BWD_MFMA
-    __shared__ float sWU[4][16 * WU_LD];
+    __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
     __shared__ unsigned short sBidx[4][MB];
 #endif
     const int tile = order[blockIdx.x];  // longest lists first (k_order)
@@ -569,7 +578,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #endif
         for (int kk = 0; kk < cnt; kk += BU) {
             int jj4[4];
-            list4(S, w, kk & ~3, jj4);
+            list_n(S, w, kk & ~3, jj4);
             int jj[BU];
 #pragma unroll
             for (int u = 0; u < BU; u++) jj[u] = jj4[(kk & 3) + u];

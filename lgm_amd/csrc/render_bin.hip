@@ -14,6 +14,8 @@
 //                      composite key (LDS blocks + global merge stages).
 #include "render_common.h"
 
+#include <type_traits>
+
 namespace lgm {
 namespace {
 
@@ -336,7 +338,12 @@ __global__ __launch_bounds__(ORD_THREADS) void k_order(int M, long long slot_str
 constexpr int RS_THREADS = LGM_RS_THREADS, RS_WAVES = RS_THREADS / 64, RS_CAP = LGM_RS_CAP,
               RS_MAXR = RS_CAP / RS_THREADS;
 constexpr int RS_DBITS = 9, RS_B = 1 << RS_DBITS;  // digit width: a typical 26-bit depth span takes 3 passes
-constexpr int RS_LDS = RS_CAP * 4 + RS_CAP * 2 + RS_WAVES * RS_B * 4;
+#ifndef LGM_RS_CNT16
+#define LGM_RS_CNT16 1  // per-wave digit counters as u16 (they never exceed RS_CAP): halves their LDS
+#endif
+typedef std::conditional<LGM_RS_CNT16, unsigned short, int>::type RsCnt;
+constexpr int RS_LDS = RS_CAP * 4 + RS_CAP * 2 + RS_WAVES * RS_B * (int)sizeof(RsCnt);
+static_assert(RS_CAP < 65536, "u16 counters");
 static_assert(RS_LDS >= RS_CAP * 8, "sort_oversized reuses the image as u64[RS_CAP]");
 static_assert(RS_B % RS_THREADS == 0 || RS_THREADS % RS_B == 0, "bucket scan layout");
 
@@ -369,10 +376,10 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
 // for the scatter. All threads of the block call it.
 __device__ __forceinline__ void radix_pass(const unsigned (&kr)[RS_MAXR], const unsigned short (&pr)[RS_MAXR],
                                           int shift, int nbits, int n, int c0, int R, unsigned *sk,
-                                          unsigned short *sp, int *cnt, int *s_wsum) {
+                                          unsigned short *sp, RsCnt *cnt, int *s_wsum) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const unsigned mask = (1u << nbits) - 1u;
-    int *my = cnt + w * RS_B;
+    RsCnt *my = cnt + w * RS_B;
     for (int q = lane; q < RS_B; q += 64) my[q] = 0;
     const unsigned long long lt = lanemask_lt(lane);
     int lr[RS_MAXR];
@@ -388,7 +395,7 @@ __device__ __forceinline__ void radix_pass(const unsigned (&kr)[RS_MAXR], const 
                 const int rk = __popcll(peers & lt);
                 const int b0 = my[dgt];  // same address for all peers: broadcast read
                 lr[r] = b0 + rk;
-                if (rk == 0) my[dgt] = b0 + __popcll(peers);
+                if (rk == 0) my[dgt] = (RsCnt)(b0 + __popcll(peers));
             }
         }
     }
@@ -411,7 +418,7 @@ __device__ __forceinline__ void radix_pass(const unsigned (&kr)[RS_MAXR], const 
         for (int j = 0; j < BPT; j++)
             for (int ww = 0; ww < RS_WAVES; ww++) {
                 const int x = cnt[ww * RS_B + tid * BPT + j];
-                cnt[ww * RS_B + tid * BPT + j] = run;
+                cnt[ww * RS_B + tid * BPT + j] = (RsCnt)run;
                 run += x;
             }
     }
@@ -508,7 +515,7 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned *sk = reinterpret_cast<unsigned *>(smem);
     unsigned short *sp = reinterpret_cast<unsigned short *>(sk + RS_CAP);
-    int *cnt = reinterpret_cast<int *>(sp + RS_CAP);
+    RsCnt *cnt = reinterpret_cast<RsCnt *>(sp + RS_CAP);
     __shared__ unsigned s_min, s_max, s_vmax;
     __shared__ int s_wsum[RS_WAVES], s_long;
     if (n <= 1) return;  // a single id already sits in place (low half of its key)
@@ -654,7 +661,10 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
 // k_sort: grid (1 + B*V*T), block RS_THREADS, dynamic LDS RS_LDS bytes. Workgroup 0 computes the LPT order
 // (it reads only the final tile counts, so it runs alongside the sorts and saves a dependent launch); workgroup
 // 1 + t sorts tile t.
-__global__ __launch_bounds__(RS_THREADS) void k_sort(int M, long long slot_stride, const int *__restrict__ tile_start,
+#ifndef LGM_RS_WPE
+#define LGM_RS_WPE 8  // minimum waves per SIMD for k_sort's registers (8: <= 64 VGPRs, 4 WGs per CU with u16 counters; 6: 80)
+#endif
+__global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_RS_WPE))) void k_sort(int M, long long slot_stride, const int *__restrict__ tile_start,
                                                      const int *__restrict__ tile_count,
                                                      unsigned long long *__restrict__ pairs, int *__restrict__ order,
                                                      unsigned long long *__restrict__ counters) {

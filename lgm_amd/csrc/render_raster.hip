@@ -12,6 +12,12 @@
 #ifndef LGM_BWD_BU
 #define LGM_BWD_BU 4  // backward entries evaluated per step (ILP vs registers): 1, 2 or 4
 #endif
+#ifndef LGM_BWD_BRANCHY
+#define LGM_BWD_BRANCHY 0  // backward serial chain with per-lane branches (1) or as selects (0)
+#endif
+#ifndef LGM_FWD_BRANCHY
+#define LGM_FWD_BRANCHY 0  // forward serial chain with per-lane branches (1) or as selects (0)
+#endif
 #ifndef LGM_FWD_FU
 #define LGM_FWD_FU 4  // forward entries evaluated per step: 4 or 8
 #endif
@@ -76,7 +82,7 @@ struct StageT {                // PAD: list padding = entries evaluated per step
     unsigned short list[4][TILE_PIX + PAD];  // per-wave compacted entry indices, padded with SENT to a multiple of PAD
 };
 #ifndef LGM_FWD_DB
-#define LGM_FWD_DB 0  // forward staging double-buffered (1) or synchronous (0): the forward usually stops early
+#define LGM_FWD_DB 0  // forward staging: 0 synchronous (measured fastest), 1 always prefetching, 2 from the second chunk
 #endif
 using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 // the backward sits 3 workgroups per CU only just: its LDS must stay <= 53,744 B (measured: 53,776 B ran at 2)
@@ -214,38 +220,31 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
     int last = 0;
     constexpr int FU = LGM_FWD_FU;
     unsigned c_iter = 0, c_acc = 0, c_list = 0;  // diagnostic work counters (Dims::counters)
-#if LGM_FWD_DB
-    // staging pipeline: chunk c+1's entries stream into the other buffer by LDS DMA while chunk c is composited;
-    // the sorted ids run one chunk further ahead in a register
-    if (tid < n) stage_dma(S.buf[0], w, ids[tid], gbase, b, d.N, gP, gQ, gauss);
-    unsigned id_next = TILE_PIX + tid < n ? ids[TILE_PIX + tid] : 0u;
+    // Staging: chunk c's entries land by LDS DMA; from chunk PF0 on (a tile that has not saturated after its first
+    // chunk is likely a long one: the critical path of the launch) chunk c+1 streams into the other buffer while c
+    // is composited. Short tiles, most of them, stage synchronously and waste no prefetch. Sorted ids run two
+    // chunks ahead in registers. Each lane tests its own entry as soon as its row has landed, so one barrier
+    // publishes rows and masks together.
+    constexpr int PF0 = LGM_FWD_DB == 1 ? 0 : 1;
+    unsigned id_a = tid < n ? ids[tid] : 0u;                        // chunk c
+    unsigned id_b = TILE_PIX + tid < n ? ids[TILE_PIX + tid] : 0u;  // chunk c + 1
     int cur = 0;
-    for (int b0 = 0; b0 < n; b0 += TILE_PIX, cur ^= 1) {
-        vm_wait_all();  // this wave's share of chunk c has landed; the barrier below publishes all four
-        if (__syncthreads_count(done) == TILE_PIX) break;
-        c_list += min(TILE_PIX, n - b0);
-        const int k = b0 + tid;
-        StageBuf &B = S.buf[cur];
-        stage_commit(S, B, tid, k < n, 0u, tx0, ty0, false);
-        __syncthreads();
-        if (k + TILE_PIX < n) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
-        id_next = k + 2 * TILE_PIX < n ? ids[k + 2 * TILE_PIX] : 0u;
-#else
-    // synchronous staging (most tiles stop within a chunk or two, so a prefetched chunk would mostly be wasted):
-    // one LDS DMA round trip per chunk, the sorted ids loaded a chunk ahead; each lane tests its own entry as soon
-    // as its row has landed, so one barrier publishes rows and masks together
-    unsigned id_cur = tid < n ? ids[tid] : 0u;
-    StageBuf &B = S.buf[0];
-    for (int b0 = 0; b0 < n; b0 += TILE_PIX) {
+    bool pre = false;  // chunk c was prefetched into S.buf[cur]
+    for (int b0 = 0, c = 0; b0 < n; b0 += TILE_PIX, c++) {
         if (__syncthreads_count(done) == TILE_PIX) break;  // also: every wave is done with the previous chunk
         c_list += min(TILE_PIX, n - b0);
         const int k = b0 + tid;
-        if (k < n) stage_dma(B, w, id_cur, gbase, b, d.N, gP, gQ, gauss);
-        id_cur = k + TILE_PIX < n ? ids[k + TILE_PIX] : 0u;
+        StageBuf &B = S.buf[cur];
+        if (!pre && k < n) stage_dma(B, w, id_a, gbase, b, d.N, gP, gQ, gauss);
         vm_wait_all();
         stage_commit(S, B, tid, k < n, 0u, tx0, ty0, false);
         __syncthreads();
-#endif
+        const bool pf = LGM_FWD_DB != 0 && c >= PF0 && b0 + TILE_PIX < n;  // workgroup-uniform
+        if (pf && k + TILE_PIX < n) stage_dma(S.buf[cur ^ 1], w, id_b, gbase, b, d.N, gP, gQ, gauss);
+        id_a = id_b;
+        id_b = k + 2 * TILE_PIX < n ? ids[k + 2 * TILE_PIX] : 0u;
+        pre = pf;
+        cur ^= pf ? 1 : 0;
         const int cnt = compact_wave(S, w, lane);
         // FU = 4 entries per step: their alphas are independent of the running transmittance, so they are evaluated
         // together (ILP, branch-free: list padded with the opacity-0 sentinel); only the short T / colour update
@@ -268,6 +267,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
                 const float alpha = fminf(0.99f, Q.y * __builtin_amdgcn_exp2f(power * LOG2E));
                 al[u] = (power > 0.0f || alpha < 1.0f / 255.0f) ? 0.f : alpha;  // 0 == skipped
             }
+#if LGM_FWD_BRANCHY
 #pragma unroll
             for (int u = 0; u < FU; u++) {
                 if (done || al[u] == 0.f) continue;
@@ -285,11 +285,29 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
                 last = b0 + jj[u] + 1;
                 c_acc++;
             }
+#else
+            // the serial chain as selects: no per-lane branches for the compiler to sink the alpha evaluations
+            // into, so the FU evaluations above stay independent (ILP across the exp latencies)
+#pragma unroll
+            for (int u = 0; u < FU; u++) {
+                const float alpha = al[u];
+                const float test_T = Tr * (1 - alpha);
+                const bool live = !done && alpha != 0.f;
+                const bool acc = live && test_T >= 0.0001f;
+                done = done || (live && !acc);
+                const float wT = acc ? Tr : 0.f;
+                C0 += cc[u].x * alpha * wT;
+                C1 += cc[u].y * alpha * wT;
+                C2 += cc[u].z * alpha * wT;
+                D += cc[u].w * alpha * wT;
+                Tr = acc ? test_T : Tr;
+                last = acc ? b0 + jj[u] + 1 : last;
+                c_acc += acc ? 1u : 0u;
+            }
+#endif
         }
     }
-#if LGM_FWD_DB
-    vm_wait_all();  // no LDS DMA may still be in flight when the workgroup retires (early termination)
-#endif
+    if (LGM_FWD_DB != 0 && pre) vm_wait_all();  // no LDS DMA may be in flight when the workgroup retires
     if (d.counters) {
         c_acc = (unsigned)__reduce_add_wave(c_acc);
         if (lane == 0) {
@@ -601,11 +619,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 al[u] = ok ? alpha : 0.f;
                 Gv[u] = Q.y;  // opacity: dL/dG = opacity * dL/dopa
                 Gg[u] = G;
-                // 1 / (1 - alpha): v_rcp_f32 + one Newton step (~0.5 ulp, like the IEEE division upstream uses)
-                const float om = 1.f - alpha;
+                // 1 / (1 - alpha): v_rcp_f32 + one Newton step (~0.5 ulp, like the IEEE division upstream uses);
+                // of the masked alpha, so a skipped entry gets exactly 1
+                const float om = 1.f - al[u];
                 float r = __builtin_amdgcn_rcpf(om);
                 inv[u] = fmaf(fmaf(-om, r, 1.0f), r, r);
             }
+#if LGM_BWD_BRANCHY
 #pragma unroll
             for (int u = 0; u < BU; u++) {
                 v[u][0] = 0.f;
@@ -642,6 +662,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 v[u][0] = Gg[u] * (Gv[u] * dL_dopa);
                 v[u][1] = alpha * Tr;  // dchannel_dcolor
             }
+#else
+            // the serial chain as selects (no per-lane branches for the compiler to sink the BU evaluations
+            // into); a skipped entry (alpha 0) leaves every recurrence unchanged: 1 / (1 - 0) == 1 exactly, and
+            // the suffix accumulators take the previous contributor with weight 0
+#pragma unroll
+            for (int u = 0; u < BU; u++) {
+                const bool valid = al[u] != 0.f;
+                const float alpha = al[u];
+                const float4 c = cc[u];
+                Tr = Tr * inv[u];
+                const float la = valid ? last_alpha : 0.f;
+                acc_r0 = fmaf(la, lc0 - acc_r0, acc_r0);
+                acc_r1 = fmaf(la, lc1 - acc_r1, acc_r1);
+                acc_r2 = fmaf(la, lc2 - acc_r2, acc_r2);
+                acc_a = fmaf(la, 1.f - acc_a, acc_a);
+                float dL_dopa = (c.x - acc_r0) * dp0;
+                dL_dopa = fmaf(c.y - acc_r1, dp1, dL_dopa);
+                dL_dopa = fmaf(c.z - acc_r2, dp2, dL_dopa);
+                if (DEPTH) {
+                    acc_d = fmaf(la, last_depth - acc_d, acc_d);
+                    dL_dopa = fmaf(c.w - acc_d, dpd, dL_dopa);
+                    last_depth = valid ? c.w : last_depth;
+                }
+                dL_dopa = fmaf(1.f - acc_a, dpa, dL_dopa);
+                dL_dopa = fmaf(dL_dopa, Tr, (-T_final * inv[u]) * bg_dot);
+                lc0 = valid ? c.x : lc0;
+                lc1 = valid ? c.y : lc1;
+                lc2 = valid ? c.z : lc2;
+                last_alpha = valid ? alpha : last_alpha;
+                v[u][0] = valid ? Gg[u] * (Gv[u] * dL_dopa) : 0.f;
+                v[u][1] = alpha * Tr;  // dchannel_dcolor (0 for a skipped entry)
+            }
+#endif
 #else
             float al[BU], Gv[BU], ex[BU], ey[BU], inv[BU];
             float4 cc[BU];

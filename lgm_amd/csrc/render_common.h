@@ -25,8 +25,10 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 //   slot mode   (pair_capacity <= 0): tile (bv, t) owns pairs[(bv*T + t) * N, +N): no counting pass, no scan.
 //   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
 struct Layout {
-    size_t gP, gQ, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, cmask, accum, misc, total;
+    size_t gP, gQ, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, cfin, ck, cklist, nck, cmask, accum,
+        misc, total;
     long long cap;
+    int ck_region;  // backward checkpoint slots per region (8 regions; the forward shards tiles over them)
     bool slot;
 };
 
@@ -41,12 +43,19 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.gQ = take(BV * N * 16);  // (C, opacity, tau, depth)
     L.rects = take(BV * N * 8);
     L.tile_count = take(BV * T * 4);
-    L.misc = take(64);  // right after tile_count: the binning clears both with one memset
+    L.misc = take(64);  // right after tile_count: the binning clears both with one memset (u64 [0..1]: pair
+                        // counts of k_bin; u32 [4..11]: the backward-checkpoint region counters)
     L.tile_start = take((BV * T + 1) * 4);
     L.order = take(BV * T * 4);
     L.pairs = take((size_t)L.cap * 8);
     L.final_T = take(BV * P * 4);
     L.n_contrib = take(BV * P * 4);
+    L.cfin = take(BV * P * 16);  // per-pixel pre-background colour and depth totals (forward -> backward)
+    // backward checkpoints (k_render_fwd -> k_render_bwd): 2 per tile on average, 5 planes of 256 floats each
+    L.ck_region = (int)((2 * BV * T + 7) / 8);
+    L.ck = take((size_t)8 * L.ck_region * 5 * TILE_PIX * 4);
+    L.cklist = take((size_t)8 * L.ck_region * 8);
+    L.nck = take(BV * T * 4);
     L.cmask = take(BV * P);
     L.accum = take(BV * N * NACC * 4);
     L.total = o;

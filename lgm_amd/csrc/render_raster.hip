@@ -162,6 +162,25 @@ __device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin 
     return cnt;
 }
 
+// compact_wave restricted to chunk entries j < jend (the backward: positions behind the wave's last contributor
+// touch none of its pixels).
+template <class Stage>
+__device__ __forceinline__ int compact_wave_below(Stage &S, int w, int lane, int jend) {
+    constexpr int PAD = (int)(sizeof(S.list[0]) / sizeof(S.list[0][0])) - TILE_PIX;
+    int cnt = 0;
+    const unsigned long long lt = lanemask_lt(lane);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int j = c * 64 + lane;
+        const bool bit = ((S.mask[j] >> w) & 1u) && j < jend;
+        const unsigned long long bal = __ballot(bit);
+        if (bit) S.list[w][cnt + __popcll(bal & lt)] = (unsigned short)j;
+        cnt += __popcll(bal);
+    }
+    if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)SENT;  // pad to the next multiple of PAD
+    return cnt;
+}
+
 // U (a multiple of 4) consecutive list entries from kk (a multiple of 4) as wave-uniform (scalar) indices.
 template <int U, class Stage>
 __device__ __forceinline__ void list_n(const Stage &S, int w, int kk, int (&jj)[U]) {
@@ -188,7 +207,10 @@ __device__ __forceinline__ void init_sentinel(Stage &S) {
 }
 
 // k_render_fwd: grid (B*V*T), block 256.
-__global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_stride, const int *__restrict__ order,
+#ifndef LGM_FWD_WPE
+#define LGM_FWD_WPE 6  // all B*V*T workgroups of the cfg3 launch are co-resident at 6 waves per SIMD (<= 80 VGPRs)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE))) void k_render_fwd(Dims d, long long slot_stride, const int *__restrict__ order,
                                                     const int *__restrict__ tile_start,
                                                     const int *__restrict__ tile_count,
                                                     const unsigned long long *__restrict__ pairs,
@@ -197,8 +219,12 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
                                                     const float *__restrict__ bg, float *__restrict__ out_img,
                                                     float *__restrict__ out_depth, float *__restrict__ out_alpha,
                                                     float *__restrict__ final_T, int *__restrict__ n_contrib,
-                                                    unsigned char *__restrict__ cmask) {
+                                                    unsigned char *__restrict__ cmask, float4 *__restrict__ cfin,
+                                                    float *__restrict__ ck, int2 *__restrict__ cklist,
+                                                    int *__restrict__ nck, unsigned *__restrict__ ckctr,
+                                                    int ck_region) {
     __shared__ StageFwd S;
+    __shared__ int s_ck[2];
     const int tile = order[blockIdx.x];  // longest lists first (k_order)
     const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
     const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
@@ -230,7 +256,14 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
     unsigned id_b = TILE_PIX + tid < n ? ids[TILE_PIX + tid] : 0u;  // chunk c + 1
     int cur = 0;
     bool pre = false;  // chunk c was prefetched into S.buf[cur]
+    // Backward checkpoints: entering every chunk c >= 1 the per-pixel state (T and the prefix colour / depth sums)
+    // goes to a pool slot, reserved one chunk ahead from the region's counter (thread 0), so that k_render_bwd can
+    // take the chunk as a work item of its own. The pool is sharded by tile over ckctr's 8 counters; a full region
+    // just leaves the rest of the tile to the previous chunk's item.
+    const int ck_reg = tile & 7;
+    int ck_slot = -1, ck_written = 0;  // thread 0: slot reserved for the next boundary; checkpoints written
     for (int b0 = 0, c = 0; b0 < n; b0 += TILE_PIX, c++) {
+        if (tid == 0) s_ck[c & 1] = ck_slot;  // reserved during chunk c - 1 (its atomic has long returned)
         if (__syncthreads_count(done) == TILE_PIX) break;  // also: every wave is done with the previous chunk
         c_list += min(TILE_PIX, n - b0);
         const int k = b0 + tid;
@@ -239,6 +272,30 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
         vm_wait_all();
         stage_commit(S, B, tid, k < n, 0u, tx0, ty0, false);
         __syncthreads();
+        // checkpoint stores and the next reservation go out after this chunk's DMA wait, so they have the whole
+        // chunk's compositing to complete before the next wait
+        if (tid == 0) {
+            ck_slot = -1;
+            if (b0 + TILE_PIX < n) {
+                const unsigned l = atomicAdd(&ckctr[ck_reg], 1u);
+                if (l < (unsigned)ck_region) ck_slot = ck_reg * ck_region + (int)l;
+            }
+        }
+        if (c >= 1) {
+            const int sl = s_ck[c & 1];  // workgroup-uniform
+            if (sl >= 0) {
+                float *cp = ck + (size_t)sl * 5 * TILE_PIX;
+                cp[tid] = Tr;
+                cp[TILE_PIX + tid] = C0;
+                cp[2 * TILE_PIX + tid] = C1;
+                cp[3 * TILE_PIX + tid] = C2;
+                cp[4 * TILE_PIX + tid] = D;
+                if (tid == 0) {
+                    cklist[sl] = make_int2(tile, c);
+                    ck_written = c;
+                }
+            }
+        }
         const bool pf = LGM_FWD_DB != 0 && c >= PF0 && b0 + TILE_PIX < n;  // workgroup-uniform
         if (pf && k + TILE_PIX < n) stage_dma(S.buf[cur ^ 1], w, id_b, gbase, b, d.N, gP, gQ, gauss);
         id_a = id_b;
@@ -255,13 +312,21 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
             int jj[FU];
             list_n(S, w, kk, jj);
             float al[FU];
-            float4 cc[FU];
+            float4 cc[FU], Pv[FU], Qv[FU];
+            // all the batch's LDS reads first, then one wait: the scheduler would otherwise interleave them with the
+            // arithmetic entry by entry (its register-pressure heuristics) and expose the LDS latency FU times
 #pragma unroll
             for (int u = 0; u < FU; u++) {
-                const float4 P = B.P[jj[u]];
-                const float4 Q = B.Q[jj[u]];
+                Pv[u] = B.P[jj[u]];
+                Qv[u] = B.Q[jj[u]];
                 const float4 R = B.R[jj[u]];
-                cc[u] = make_float4(R.x, R.y, R.z, Q.w);
+                cc[u] = make_float4(R.x, R.y, R.z, 0.f);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < FU; u++) {
+                const float4 P = Pv[u], Q = Qv[u];
+                cc[u].w = Q.w;
                 const float dx = P.x - pfx, dy = P.y - pfy;
                 const float power = -0.5f * (P.z * dx * dx + Q.x * dy * dy) - P.w * dx * dy;
                 const float alpha = fminf(0.99f, Q.y * __builtin_amdgcn_exp2f(power * LOG2E));
@@ -295,19 +360,25 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
                 const bool live = !done && alpha != 0.f;
                 const bool acc = live && test_T >= 0.0001f;
                 done = done || (live && !acc);
-                const float wT = acc ? Tr : 0.f;
-                C0 += cc[u].x * alpha * wT;
-                C1 += cc[u].y * alpha * wT;
-                C2 += cc[u].z * alpha * wT;
-                D += cc[u].w * alpha * wT;
+                const float aw = acc ? alpha * Tr : 0.f;
+                C0 = fmaf(cc[u].x, aw, C0);
+                C1 = fmaf(cc[u].y, aw, C1);
+                C2 = fmaf(cc[u].z, aw, C2);
+                D = fmaf(cc[u].w, aw, D);
                 Tr = acc ? test_T : Tr;
                 last = acc ? b0 + jj[u] + 1 : last;
+#ifdef LGM_WORK_COUNTERS
                 c_acc += acc ? 1u : 0u;
+#endif
             }
 #endif
         }
     }
     if (LGM_FWD_DB != 0 && pre) vm_wait_all();  // no LDS DMA may be in flight when the workgroup retires
+    if (tid == 0) {
+        if (ck_slot >= 0) cklist[ck_slot] = make_int2(-1, 0);  // reserved for a boundary never reached
+        nck[tile] = ck_written;  // checkpoints c = 1 .. ck_written exist (a prefix: the counters only grow)
+    }
     if (d.counters) {
         c_acc = (unsigned)__reduce_add_wave(c_acc);
         if (lane == 0) {
@@ -340,6 +411,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(Dims d, long long slot_strid
         img[2 * P + pid] = c2;
         out_depth[bv * P + pid] = D;
         out_alpha[bv * P + pid] = 1 - Tr;
+        cfin[bv * P + pid] = make_float4(C0, C1, C2, D);  // pre-background totals for the backward
     }
 }
 
@@ -354,34 +426,59 @@ __device__ __forceinline__ float row_sum16(float v) {
     return v;
 }
 
-// k_render_bwd: grid (B*V*T), block 256. DEPTH: an upstream depth gradient is present (LGM passes none).
+// k_render_bwd: grid (B*V*T + CK slots), block 256. DEPTH: an upstream depth gradient is present (LGM passes none).
+//
+// The gradient pass walks each tile's list FRONT TO BACK, the forward's order. Upstream's reverse recurrence (suffix
+// colour accumulators) is replaced by the equivalent prefix form: with T_i the transmittance in front of entry i,
+// D_i = sum_{j <= i} alpha_j T_j (c_j . dL/dC) and the forward's per-pixel totals Dfin = C . dL/dC, T_final,
+//     dL/dalpha_i = T_i (c_i . dL/dC) - (Dfin - K - D_i) / (1 - alpha_i),    K = (dL/dA - bg . dL/dC) T_final,
+// so the per-pixel state is just (T, D). That state is what the forward checkpoints at each 256-entry chunk
+// boundary it crosses (k_render_fwd: T and the prefix colour/depth sums; D = prefix . dL/dC), so the backward work
+// item is one CHUNK, not one tile: workgroup g < B*V*T takes chunk 0 of LPT tile g, workgroup B*V*T + s takes the
+// chunk of checkpoint slot s (cklist), and runs to the next checkpoint (or the tile's end if the pool ran out).
+// Long tiles no longer bound the launch.
+//
+// Per-entry gradient sums over a wave's 64 pixels are pixel moments on the MFMA: w = G dL/dG and u = alpha T give
+// sum_p w f(p) for f in {1, x, y, x^2, xy, y^2} (tile-centred pixel coordinates; the mean2D and conic partials
+// follow from these and the Gaussian centre) and sum_p u dL/dC_c(p): a [features x pixels] . [pixels x entries]
+// product, MB entries' w (columns 0..MB-1) and u (columns MB..) written to a per-wave LDS image and summed by
+// v_mfma_f32_16x16x32_bf16 (the geometric features are exact in bf16; w, u and dL/dC as hi + lo bf16 pairs, ~2^-16
+// relative per product). Moments are combined over the tile's four waves in LDS, turned into gradient partials per
+// entry and flushed once per (chunk, entry) to the per-view accumulators.
 #ifndef LGM_BWD_WPE
 #define LGM_BWD_WPE 3  // minimum waves per SIMD the register allocation must allow (4: <= 128 VGPRs)
 #endif
 template <bool DEPTH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 : LGM_BWD_WPE))) void k_render_bwd(Dims d, long long slot_stride, const int *__restrict__ order,
-                                                    const int *__restrict__ tile_start,
-                                                    const int *__restrict__ tile_count,
-                                                    const unsigned long long *__restrict__ pairs,
-                                                    const float4 *__restrict__ gP, const float4 *__restrict__ gQ,
-                                                    const float *__restrict__ gauss,
-                                                    const float *__restrict__ bg, const float *__restrict__ final_T,
-                                                    const int *__restrict__ n_contrib,
-                                                    const float *__restrict__ d_img,
-                                                    const float *__restrict__ d_depth,
-                                                    const float *__restrict__ d_alpha,
-                                                    const unsigned char *__restrict__ cmask,
-                                                    float *__restrict__ accum) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 : LGM_BWD_WPE))) void k_render_bwd(
+    Dims d, long long slot_stride, const int *__restrict__ order, const int *__restrict__ tile_start,
+    const int *__restrict__ tile_count, const unsigned long long *__restrict__ pairs, const float4 *__restrict__ gP,
+    const float4 *__restrict__ gQ, const float *__restrict__ gauss, const float *__restrict__ bg,
+    const float *__restrict__ final_T, const int *__restrict__ n_contrib, const float4 *__restrict__ cfin,
+    const float *__restrict__ ck, const int2 *__restrict__ cklist, const int *__restrict__ nck,
+    const unsigned *__restrict__ ckctr, int ck_region, const float *__restrict__ d_img,
+    const float *__restrict__ d_depth, const float *__restrict__ d_alpha, const unsigned char *__restrict__ cmask,
+    float *__restrict__ accum) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
     constexpr int LS = TILE_PIX + 1;             // padded LDS row stride (no bank conflicts)
     __shared__ StageBwd S;
     __shared__ __attribute__((aligned(16))) float sAcc[LS * NV];  // 9 rows without a depth gradient
     __shared__ int sMaxLast;
-#if LGM_BWD_MFMA
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
     __shared__ unsigned short sBidx[4][MB];
-#endif
-    const int tile = order[blockIdx.x];  // longest lists first (k_order)
+    // ---- work item: (tile, chunk c, checkpoint slot)
+    const int M = d.BV * d.T;
+    int tile, c = 0, slot = -1;
+    if ((int)blockIdx.x < M) {
+        tile = order[blockIdx.x];  // longest lists first (k_order)
+    } else {
+        slot = (int)blockIdx.x - M;
+        const int region = slot / ck_region;
+        if (slot - region * ck_region >= (int)ckctr[region]) return;  // an unused slot (workgroup-uniform)
+        const int2 e = cklist[slot];
+        if (e.x < 0) return;  // reserved, never written
+        tile = e.x;
+        c = e.y;
+    }
     const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
     const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -399,6 +496,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const float T_final = inside ? final_T[bv * P + pid] : 0.f;
     const int last = inside ? n_contrib[bv * P + pid] : 0;
     float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, dpd = 0.f, dpa = 0.f;
+    float4 cf = make_float4(0.f, 0.f, 0.f, 0.f);
     if (inside) {
         const float *di = d_img + (size_t)bv * 3 * P;
         dp0 = di[pid];
@@ -412,36 +510,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         }
         if (DEPTH) dpd = d_depth[bv * P + pid];
         if (d_alpha) dpa = d_alpha[bv * P + pid];
+        cf = cfin[bv * P + pid];
     }
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    // per-pixel state entering the chunk: the forward's checkpoint (or the list head)
+    float Tr = 1.0f, Dup = 0.f;
+    if (slot >= 0) {
+        const float *cp = ck + (size_t)slot * 5 * TILE_PIX;
+        Tr = cp[tid];
+        Dup = fmaf(cp[TILE_PIX + tid], dp0, fmaf(cp[2 * TILE_PIX + tid], dp1, cp[3 * TILE_PIX + tid] * dp2));
+        if (DEPTH) Dup = fmaf(cp[4 * TILE_PIX + tid], dpd, Dup);
+    }
     init_sentinel(S);
     if (tid == 0) sMaxLast = 0;
     __syncthreads();
-    const int wlast = wave_max_i32(last);  // entries at positions >= wlast touch no pixel of this wave
+    const int wlast = wave_max_i32(last);  // positions >= wlast touch no pixel of this wave
     if (lane == 0 && wlast > 0) atomicMax(&sMaxLast, wlast);
     __syncthreads();
     const int nlist = min(n, sMaxLast);  // entries behind every pixel's last contributor are never visited
-    if (nlist == 0) return;
+    const int s0 = c * TILE_PIX;
+    if (s0 >= nlist) return;  // workgroup-uniform
+    const int s1 = (c + 1 <= nck[tile]) ? min(nlist, s0 + TILE_PIX) : nlist;
     const float bg_dot = bg[0] * dp0 + bg[1] * dp1 + bg[2] * dp2;
+    float cdpf = fmaf(cf.x, dp0, fmaf(cf.y, dp1, cf.z * dp2));
+    if (DEPTH) cdpf = fmaf(cf.w, dpd, cdpf);
+    const float DK = cdpf - (dpa - bg_dot) * T_final;  // Dfin - K
     const float ddelx_dx = 0.5f * d.W, ddely_dy = 0.5f * d.H;
-    float Tr = T_final;
-    float acc_r0 = 0, acc_r1 = 0, acc_r2 = 0, acc_d = 0, acc_a = 0;
-    float last_alpha = 0, lc0 = 0, lc1 = 0, lc2 = 0, last_depth = 0;
     const size_t gbase = (size_t)bv * d.N;
-    const int ql = lane & 15;
     constexpr int BU = LGM_BWD_BU;
-    unsigned c_iter = 0, c_valid = 0, c_dense = 0, c_sparse = 0;
-#ifdef LGM_BWD_STAMPS
-    unsigned long long sec_stage = 0, sec_compact = 0, sec_loop = 0, sec_flush = 0, sec_tail = 0;
-#endif
-#if LGM_BWD_MFMA
-    // Every per-entry gradient sum over the wave's 64 pixels is a pixel moment of two per-(pixel, entry) scalars,
-    // w = G dL/dG and u = alpha T: sum_p w f(p) for f in {1, x, y, x^2, xy, y^2} (tile-centred pixel
-    // coordinates; mean2D and conic partials follow from these and the Gaussian centre) and sum_p u dL/dC_c(p).
-    // So the reduction is the product [features x pixels] . [pixels x entries]: MB entries' w (columns 0..MB-1)
-    // and u (columns MB..) are written to a per-wave LDS image and summed by 16 exact-f32 v_mfma_f32_16x16x4_f32
-    // over the 64 pixels. A operand: lane (ql, qk) holds feature ql of wave pixel 4s + qk, s = 0..15.
-    const int qk = lane >> 4;
+    // MFMA operands: A (features) lane (ql, qk) holds feature ql of wave pixels 32 t + 8 qk + j, j = 0..7
+    const int ql = lane & 15, qk = lane >> 4;
     const float cxT = (float)tx0 + 7.5f, cyT = (float)ty0 + 7.5f;
     float *myWU = sWU[w];
     myWU[lane] = dp0;
@@ -449,10 +546,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     myWU[128 + lane] = dp2;
     myWU[192 + lane] = dpd;
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#if LGM_BWD_MFMA == 2
-    // A operand of v_mfma_f32_16x16x32_bf16: lane (ql, qk) holds feature ql of pixels 32 t + 8 qk + j, j = 0..7.
-    // The geometric features (half-integer tile coordinates and their products, |f| <= 56.25) are exact in bf16;
-    // the upstream-gradient features get a hi + lo split.
     bf16x8 Ah[2], Al[2];
 #pragma unroll
     for (int t2 = 0; t2 < 2; t2++) {
@@ -475,32 +568,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             Al[t2][j] = (__bf16)(f - (float)h);
         }
     }
-#else
-    float Af[16];
-#pragma unroll
-    for (int s4 = 0; s4 < 16; s4++) {
-        const int p = 4 * s4 + qk;
-        int lx2, ly2;
-        tile_pixel(w * 64 + p, lx2, ly2);
-        const float fx = (float)(tx0 + lx2) - cxT, fy = (float)(ty0 + ly2) - cyT;
-        float f = 0.f;
-        if (ql == 0) f = 1.f;
-        else if (ql == 1) f = fx;
-        else if (ql == 2) f = fy;
-        else if (ql == 3) f = fx * fx;
-        else if (ql == 4) f = fx * fy;
-        else if (ql == 5) f = fy * fy;
-        else if (ql <= 9) f = myWU[(ql - 6) * 64 + p];
-        Af[s4] = f;
-    }
-#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     auto flush_batch = [&](int nb) {
-#ifdef LGM_TIMING_SKIP_FLUSH  // timing-only diagnostic build: wrong gradients
-        return;
-#endif
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#if LGM_BWD_MFMA == 2
         // B operand: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t), split hi + lo
         f32x4 a2[2];
 #pragma unroll
@@ -515,25 +585,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 bh[j] = h;
                 bl[j] = (__bf16)(xs[j] - (float)h);
             }
-            f32x4 c = {0.f, 0.f, 0.f, 0.f};
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al[t2], bh, c, 0, 0, 0);
-            a2[t2] = c;
+            f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
+            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);
+            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, cacc, 0, 0, 0);
+            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al[t2], bh, cacc, 0, 0, 0);
+            a2[t2] = cacc;
         }
         const f32x4 acc = a2[0] + a2[1];
-#else
-        // operands read up front (one LDS round trip), two accumulation chains (dependent-issue latency ~40 cyc)
-        float bq[16];
-#pragma unroll
-        for (int s4 = 0; s4 < 16; s4++) bq[s4] = myWU[ql * WU_LD + 4 * s4 + qk];
-        __builtin_amdgcn_sched_barrier(0);
-        f32x4 a2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-        for (int s4 = 0; s4 < 16; s4++)
-            a2[s4 & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[s4], bq[s4], a2[s4 & 1], 0, 0, 0);
-        const f32x4 acc = a2[0] + a2[1];
-#endif
         // D[row = 4 qk + r][col = ql]: moments 0..5 in w columns, rows 6..9 in u columns
         if (ql < MB) {
             if (ql < nb) {
@@ -560,249 +618,93 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     };
-#endif
 
-    // Staging pipeline (the list walked back to front): chunk c+1 streams into the other buffer by LDS DMA during
-    // chunk c's compositing, and is complete (vm_wait_all) before chunk c's gradient atomics are issued, so no
-    // staging load ever queues behind them; the sorted ids run one chunk further ahead in a register.
-    unsigned id_cur = tid < nlist ? ids[nlist - 1 - tid] : 0u;
-    if (tid < nlist) stage_dma(S.buf[0], w, id_cur, gbase, b, d.N, gP, gQ, gauss);
-    unsigned id_next = TILE_PIX + tid < nlist ? ids[nlist - 1 - TILE_PIX - tid] : 0u;
+    // Staging pipeline (front to back over [s0, s1)): chunk b0 + 256 streams into the other buffer by LDS DMA
+    // during chunk b0's compositing and is complete (vm_wait_all) before chunk b0's gradient atomics are issued,
+    // so no staging load queues behind them; the sorted ids run one chunk further ahead in a register.
+    unsigned id_cur = s0 + tid < s1 ? ids[s0 + tid] : 0u;
+    if (s0 + tid < s1) stage_dma(S.buf[0], w, id_cur, gbase, b, d.N, gP, gQ, gauss);
+    unsigned id_next = s0 + TILE_PIX + tid < s1 ? ids[s0 + TILE_PIX + tid] : 0u;
     vm_wait_all();
     int cur = 0;
-    for (int b0 = 0; b0 < nlist; b0 += TILE_PIX, cur ^= 1) {
-        SEC_T(ts0);
+    for (int b0 = s0; b0 < s1; b0 += TILE_PIX, cur ^= 1) {
         __syncthreads();
-        const int k = b0 + tid;  // counted from the back
+        const int k = b0 + tid;
         StageBuf &B = S.buf[cur];
-        stage_commit(S, B, tid, k < nlist, id_cur, tx0, ty0, true);
+        stage_commit(S, B, tid, k < s1, id_cur, tx0, ty0, true);
 #pragma unroll
         for (int q = 0; q < NV; q++) sAcc[q * LS + tid] = 0.f;
         __syncthreads();
-        if (k + TILE_PIX < nlist) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
+        if (k + TILE_PIX < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
         id_cur = id_next;
-        id_next = k + 2 * TILE_PIX < nlist ? ids[nlist - 1 - (k + 2 * TILE_PIX)] : 0u;
-        SEC_T(ts1);
-        SEC_ADD(sec_stage, ts0, ts1);
-        // position nlist - 1 - (b0 + j) < wlast  <=>  j >= nlist - wlast - b0
-        const int cnt = compact_wave(S, w, lane, nlist - wlast - b0);
-        SEC_T(ts2);
-        SEC_ADD(sec_compact, ts1, ts2);
-        c_iter += cnt;
-        // BU entries per step: G, alpha and the G-derivatives are independent of the per-pixel recurrences, so
-        // they are evaluated together (ILP); the T / suffix-accumulator recurrences stay serial in list order.
-#if LGM_BWD_MFMA
+        id_next = k + 2 * TILE_PIX < s1 ? ids[k + 2 * TILE_PIX] : 0u;
+        const int cnt = compact_wave_below(S, w, lane, wlast - b0);  // positions < wlast only
         int nb = 0;  // entries in the pending MFMA batch (wave-uniform)
-#endif
         for (int kk = 0; kk < cnt; kk += BU) {
             int jj4[4];
             list_n(S, w, kk & ~3, jj4);
             int jj[BU];
 #pragma unroll
             for (int u = 0; u < BU; u++) jj[u] = jj4[(kk & 3) + u];
-#if LGM_BWD_MFMA
-            float al[BU], Gv[BU], Gg[BU], inv[BU];
-            float4 cc[BU];
+            float al[BU], Gw[BU];
+            float4 cc[BU], Pv[BU], Qv[BU];
+#pragma unroll
+            for (int u = 0; u < BU; u++) {  // the batch's LDS reads first, one wait (see k_render_fwd)
+                Pv[u] = B.P[jj[u]];
+                Qv[u] = B.Q[jj[u]];
+                const float4 Rj = B.R[jj[u]];
+                cc[u] = make_float4(Rj.x, Rj.y, Rj.z, 0.f);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < BU; u++) {
+                const int pos = b0 + jj[u];  // 0-based position in the tile list
+                const float4 Pj = Pv[u], Q = Qv[u];
+                cc[u].w = Q.w;
+                const float dx = Pj.x - pfx, dy = Pj.y - pfy;
+                const float power = -0.5f * (Pj.z * dx * dx + Q.x * dy * dy) - Pj.w * dx * dy;
+                const float G = __builtin_amdgcn_exp2f(power * LOG2E);
+                const float alpha = fminf(0.99f, Q.y * G);
+                const bool ok = pos < last && power <= 0.0f && alpha >= 1.0f / 255.0f;
+                al[u] = ok ? alpha : 0.f;
+                Gw[u] = G * Q.y;  // dL/dG = opacity dL/dalpha
+            }
+            // the prefix recurrences in list order (a skipped entry, alpha 0, leaves T and D unchanged)
             float v[BU][2];  // w = G dL/dG, u = alpha T
 #pragma unroll
             for (int u = 0; u < BU; u++) {
-                const int pos = nlist - 1 - (b0 + jj[u]);  // 0-based position in the tile list
-                const float4 Pj = B.P[jj[u]];
-                const float4 Q = B.Q[jj[u]];
-                const float4 Rj = B.R[jj[u]];
-                cc[u] = make_float4(Rj.x, Rj.y, Rj.z, Q.w);
-                const float dx = Pj.x - pfx, dy = Pj.y - pfy;
-                const float power = -0.5f * (Pj.z * dx * dx + Q.x * dy * dy) - Pj.w * dx * dy;
-                const float G = __builtin_amdgcn_exp2f(power * LOG2E);
-                const float alpha = fminf(0.99f, Q.y * G);
-                const bool ok = pos < last && power <= 0.0f && alpha >= 1.0f / 255.0f;
-                al[u] = ok ? alpha : 0.f;
-                Gv[u] = Q.y;  // opacity: dL/dG = opacity * dL/dopa
-                Gg[u] = G;
-                // 1 / (1 - alpha): v_rcp_f32 + one Newton step (~0.5 ulp, like the IEEE division upstream uses);
-                // of the masked alpha, so a skipped entry gets exactly 1
-                const float om = 1.f - al[u];
-                float r = __builtin_amdgcn_rcpf(om);
-                inv[u] = fmaf(fmaf(-om, r, 1.0f), r, r);
-            }
-#if LGM_BWD_BRANCHY
-#pragma unroll
-            for (int u = 0; u < BU; u++) {
-                v[u][0] = 0.f;
-                v[u][1] = 0.f;
-                if (al[u] == 0.f) continue;
-#ifdef LGM_TIMING_SKIP_SERIAL  // timing-only diagnostic build: wrong gradients
-                v[u][0] = Gg[u];
-                v[u][1] = al[u];
-                continue;
-#endif
                 const float alpha = al[u];
-                const float4 c = cc[u];
-                Tr = Tr * inv[u];
-                float dL_dopa = 0.f;
-                acc_r0 = last_alpha * lc0 + (1.f - last_alpha) * acc_r0;
-                lc0 = c.x;
-                dL_dopa += (c.x - acc_r0) * dp0;
-                acc_r1 = last_alpha * lc1 + (1.f - last_alpha) * acc_r1;
-                lc1 = c.y;
-                dL_dopa += (c.y - acc_r1) * dp1;
-                acc_r2 = last_alpha * lc2 + (1.f - last_alpha) * acc_r2;
-                lc2 = c.z;
-                dL_dopa += (c.z - acc_r2) * dp2;
-                if (DEPTH) {
-                    acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
-                    last_depth = c.w;
-                    dL_dopa += (c.w - acc_d) * dpd;
-                }
-                acc_a = last_alpha + (1.f - last_alpha) * acc_a;
-                dL_dopa += (1 - acc_a) * dpa;
-                dL_dopa *= Tr;
-                last_alpha = alpha;
-                dL_dopa += (-T_final * inv[u]) * bg_dot;
-                v[u][0] = Gg[u] * (Gv[u] * dL_dopa);
-                v[u][1] = alpha * Tr;  // dchannel_dcolor
-            }
-#else
-            // the serial chain as selects (no per-lane branches for the compiler to sink the BU evaluations
-            // into); a skipped entry (alpha 0) leaves every recurrence unchanged: 1 / (1 - 0) == 1 exactly, and
-            // the suffix accumulators take the previous contributor with weight 0
-#pragma unroll
-            for (int u = 0; u < BU; u++) {
-                const bool valid = al[u] != 0.f;
-                const float alpha = al[u];
-                const float4 c = cc[u];
-                Tr = Tr * inv[u];
-                const float la = valid ? last_alpha : 0.f;
-                acc_r0 = fmaf(la, lc0 - acc_r0, acc_r0);
-                acc_r1 = fmaf(la, lc1 - acc_r1, acc_r1);
-                acc_r2 = fmaf(la, lc2 - acc_r2, acc_r2);
-                acc_a = fmaf(la, 1.f - acc_a, acc_a);
-                float dL_dopa = (c.x - acc_r0) * dp0;
-                dL_dopa = fmaf(c.y - acc_r1, dp1, dL_dopa);
-                dL_dopa = fmaf(c.z - acc_r2, dp2, dL_dopa);
-                if (DEPTH) {
-                    acc_d = fmaf(la, last_depth - acc_d, acc_d);
-                    dL_dopa = fmaf(c.w - acc_d, dpd, dL_dopa);
-                    last_depth = valid ? c.w : last_depth;
-                }
-                dL_dopa = fmaf(1.f - acc_a, dpa, dL_dopa);
-                dL_dopa = fmaf(dL_dopa, Tr, (-T_final * inv[u]) * bg_dot);
-                lc0 = valid ? c.x : lc0;
-                lc1 = valid ? c.y : lc1;
-                lc2 = valid ? c.z : lc2;
-                last_alpha = valid ? alpha : last_alpha;
-                v[u][0] = valid ? Gg[u] * (Gv[u] * dL_dopa) : 0.f;
-                v[u][1] = alpha * Tr;  // dchannel_dcolor (0 for a skipped entry)
-            }
-#endif
-#else
-            float al[BU], Gv[BU], ex[BU], ey[BU], inv[BU];
-            float4 cc[BU];
-            float v[BU][NACC];
-#pragma unroll
-            for (int u = 0; u < BU; u++) {
-                al[u] = 0.f;
-#pragma unroll
-                for (int q = 0; q < NACC; q++) v[u][q] = 0.f;
-                const int pos = nlist - 1 - (b0 + jj[u]);  // 0-based position in the tile list
-                const float4 Pj = B.P[jj[u]];
-                const float4 Q = B.Q[jj[u]];
-                const float4 Rj = B.R[jj[u]];
-                cc[u] = make_float4(Rj.x, Rj.y, Rj.z, Q.w);
-                const float dx = Pj.x - pfx, dy = Pj.y - pfy;
-                const float power = -0.5f * (Pj.z * dx * dx + Q.x * dy * dy) - Pj.w * dx * dy;
-                const float G = __builtin_amdgcn_exp2f(power * LOG2E);
-                const float alpha = fminf(0.99f, Q.y * G);
-                const bool ok = pos < last && power <= 0.0f && alpha >= 1.0f / 255.0f;
-                al[u] = ok ? alpha : 0.f;
-                Gv[u] = Q.y;  // opacity: dL/dG = opacity * dL/dopa
-                const float gdx = G * dx, gdy = G * dy;
-                // dG/d(mean2D) in pixels, and the conic partials share these
-                ex[u] = -gdx * Pj.z - gdy * Pj.w;
-                ey[u] = -gdy * Q.x - gdx * Pj.w;
-                v[u][2] = -0.5f * gdx * dx;  // scaled by dL/dG below
-                v[u][3] = -0.5f * gdx * dy;
-                v[u][4] = -0.5f * gdy * dy;
-                v[u][5] = G;  // scaled by dL/dopa below
-                // 1 / (1 - alpha): v_rcp_f32 + one Newton step (~0.5 ulp, like the IEEE division upstream uses)
+                const float4 cu = cc[u];
+                float cdp = fmaf(cu.x, dp0, fmaf(cu.y, dp1, cu.z * dp2));
+                if (DEPTH) cdp = fmaf(cu.w, dpd, cdp);
+                const float aT = alpha * Tr;
+                Dup = fmaf(aT, cdp, Dup);
                 const float om = 1.f - alpha;
-                float r = __builtin_amdgcn_rcpf(om);
-                inv[u] = fmaf(fmaf(-om, r, 1.0f), r, r);
+                const float r0 = __builtin_amdgcn_rcpf(om);
+                const float inv = fmaf(fmaf(-om, r0, 1.0f), r0, r0);  // 1 / (1 - alpha), ~0.5 ulp
+                const float dL_dalpha = fmaf(Tr, cdp, -(DK - Dup) * inv);
+                Tr = Tr - aT;
+                v[u][0] = alpha != 0.f ? Gw[u] * dL_dalpha : 0.f;
+                v[u][1] = aT;  // dchannel_dcolor (0 for a skipped entry)
             }
-#pragma unroll
-            for (int u = 0; u < BU; u++) {
-                if (al[u] == 0.f) {
-#pragma unroll
-                    for (int q = 0; q < NACC; q++) v[u][q] = 0.f;
-                    continue;
-                }
-                const float alpha = al[u];
-                const float4 c = cc[u];
-                Tr = Tr * inv[u];
-                const float dchannel_dcolor = alpha * Tr;
-                float dL_dopa = 0.f;
-                acc_r0 = last_alpha * lc0 + (1.f - last_alpha) * acc_r0;
-                lc0 = c.x;
-                dL_dopa += (c.x - acc_r0) * dp0;
-                acc_r1 = last_alpha * lc1 + (1.f - last_alpha) * acc_r1;
-                lc1 = c.y;
-                dL_dopa += (c.y - acc_r1) * dp1;
-                acc_r2 = last_alpha * lc2 + (1.f - last_alpha) * acc_r2;
-                lc2 = c.z;
-                dL_dopa += (c.z - acc_r2) * dp2;
-                v[u][6] = dchannel_dcolor * dp0;
-                v[u][7] = dchannel_dcolor * dp1;
-                v[u][8] = dchannel_dcolor * dp2;
-                if (DEPTH) {
-                    acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
-                    last_depth = c.w;
-                    dL_dopa += (c.w - acc_d) * dpd;
-                    v[u][9] = dchannel_dcolor * dpd;
-                }
-                acc_a = last_alpha + (1.f - last_alpha) * acc_a;
-                dL_dopa += (1 - acc_a) * dpa;
-                dL_dopa *= Tr;
-                last_alpha = alpha;
-                dL_dopa += (-T_final * inv[u]) * bg_dot;
-                const float dL_dG = Gv[u] * dL_dopa;
-                v[u][0] = dL_dG * ex[u] * ddelx_dx;
-                v[u][1] = dL_dG * ey[u] * ddely_dy;
-                v[u][2] *= dL_dG;
-                v[u][3] *= dL_dG;
-                v[u][4] *= dL_dG;
-                v[u][5] *= dL_dopa;
-            }
-#endif
-#if LGM_BWD_MFMA
 #pragma unroll
             for (int u = 0; u < BU; u++) {
                 const bool valid = al[u] != 0.f;
                 const unsigned long long bal = __ballot(valid);  // wave-uniform
                 if (bal == 0ull) continue;
-                c_valid += __popcll(bal);
-                myWU[nb * WU_LD + lane] = valid ? v[u][0] : 0.f;        // w
-                myWU[(MB + nb) * WU_LD + lane] = valid ? v[u][1] : 0.f; // u
+                myWU[nb * WU_LD + lane] = v[u][0];         // w
+                myWU[(MB + nb) * WU_LD + lane] = v[u][1];  // u
                 if (lane == 0) sBidx[w][nb] = (unsigned short)jj[u];
                 if (++nb == MB) {
-                    c_dense++;
-                    SEC_T(tf0);
                     flush_batch(MB);
-                    SEC_T(tf1);
-                    SEC_ADD(sec_flush, tf0, tf1);
                     nb = 0;
                 }
             }
         }
-        SEC_T(ts3);
-        SEC_ADD(sec_loop, ts2, ts3);
-        if (nb) {
-            c_sparse++;
-            flush_batch(nb);
-            nb = 0;
-        }
+        if (nb) flush_batch(nb);
         __syncthreads();
         // moments -> gradient partials, in place (one thread per staged entry)
-        if (b0 + tid < nlist) {
+        if (b0 + tid < s1) {
             const int j = tid;
             const float4 Pj = B.P[j];
             const float4 Qj = B.Q[j];
@@ -822,74 +724,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             sAcc[5 * LS + j] = Qj.y > 0.f ? q[0] / Qj.y : 0.f;
             // [6..9] colour / depth sums are already the partials
         }
-#else
-#pragma unroll
-            for (int u = 0; u < BU; u++) {
-                const bool valid = al[u] != 0.f;
-                const unsigned long long bal = __ballot(valid);  // wave-uniform
-                if (bal == 0ull) continue;
-                c_valid += __popcll(bal);
-                const int j = jj[u];
-                if (__popcll(bal) <= 4) {  // sparse: the few active lanes add directly
-                    c_sparse++;
-                    if (valid) {
-#pragma unroll
-                        for (int q = 0; q < NV; q++) atomicAdd(&sAcc[q * LS + j], v[u][q]);
-                    }
-                } else {  // dense: 16-lane DPP row sums, then lane (row, q) adds value q: one ds_add per entry
-                    c_dense++;
-                    float mine = 0.f;
-#pragma unroll
-                    for (int q = 0; q < NV; q++) {
-                        const float rr = row_sum16(v[u][q]);
-                        mine = (ql == q) ? rr : mine;
-                    }
-                    if (ql < NV) atomicAdd(&sAcc[ql * LS + j], mine);
-                }
-            }
-        }
-#endif
-        vm_wait_all();  // chunk c+1's DMA and ids have landed: the atomics below cannot delay them
+        vm_wait_all();  // the next chunk's DMA and ids have landed: the atomics below cannot delay them
         __syncthreads();
-#ifdef LGM_BWD_STAMPS
-        struct TailStamp {
-            unsigned long long t0, &acc;
-            __device__ ~TailStamp() { acc += sec_stamp() - t0; }
-        } tail_stamp{ts3, sec_tail};
-#endif
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
 #pragma unroll
         for (int it = 0; it < NACC; it++) {
             const int f = it * TILE_PIX + tid;
             const int j = f / NACC, q = f - j * NACC;
-            if (q < NV && b0 + j < nlist) {
+            if (q < NV && b0 + j < s1) {
                 const float a = sAcc[q * LS + j];
-#ifndef LGM_TIMING_SKIP_ATOMICS  // timing-only diagnostic build: wrong gradients
                 if (a != 0.f) atomicAdd(accum + (gbase + reinterpret_cast<const unsigned *>(&B.R[j])[3]) * NACC + q, a);
-#endif
             }
         }
-    }
-#ifdef LGM_BWD_STAMPS
-    if (d.counters && lane == 0) {  // shader-clock cycles per section, summed over waves: counters [2..6]
-        atomicAdd(&d.counters[2], sec_stage);
-        atomicAdd(&d.counters[3], sec_compact);
-        atomicAdd(&d.counters[4], sec_loop - sec_flush);
-        atomicAdd(&d.counters[5], sec_flush);
-        atomicAdd(&d.counters[6], sec_tail);
-    }
-    if (d.counters) return;
-#endif
-    if (d.counters && tid == 0) {
-        d.counters[8 + 8 * (size_t)tile + 2] = t_start;
-        d.counters[8 + 8 * (size_t)tile + 3] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (d.counters && lane == 0) {
-        atomicAdd(&d.counters[2], (unsigned long long)c_iter);
-        atomicAdd(&d.counters[3], (unsigned long long)c_valid);
-        atomicAdd(&d.counters[4], (unsigned long long)c_dense);
-        atomicAdd(&d.counters[5], (unsigned long long)c_sparse);
     }
 }
 
@@ -1037,7 +884,9 @@ int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, fl
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
                                        image, depth, alpha,
                                        (float *)(ws + L.final_T), (int *)(ws + L.n_contrib),
-                                       (unsigned char *)(ws + L.cmask))));
+                                       (unsigned char *)(ws + L.cmask), (float4 *)(ws + L.cfin),
+                                       (float *)(ws + L.ck), (int2 *)(ws + L.cklist), (int *)(ws + L.nck),
+                                       (unsigned *)(ws + L.misc) + 4, L.ck_region)));
     return LGM_OK;
 }
 
@@ -1045,14 +894,16 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
                       const float *bg, const float *d_image, const float *d_depth, const float *d_alpha,
                       float *d_gaussians, float *d_means2D, char *ws, const Layout &L, hipStream_t st) {
     auto bwd = d_depth ? k_render_bwd<true> : k_render_bwd<false>;
-    LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
+    // work items: chunk 0 of every tile, then one per checkpoint slot (unused slots exit at once)
+    LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(d.BV * d.T + 8 * L.ck_region), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
-                                       (const float *)(ws + L.final_T),
-                                       (const int *)(ws + L.n_contrib), d_image, d_depth, d_alpha,
-                                       (const unsigned char *)(ws + L.cmask),
-                                       (float *)(ws + L.accum))));
+                                       (const float *)(ws + L.final_T), (const int *)(ws + L.n_contrib),
+                                       (const float4 *)(ws + L.cfin), (const float *)(ws + L.ck),
+                                       (const int2 *)(ws + L.cklist), (const int *)(ws + L.nck),
+                                       (const unsigned *)(ws + L.misc) + 4, L.ck_region, d_image, d_depth, d_alpha,
+                                       (const unsigned char *)(ws + L.cmask), (float *)(ws + L.accum))));
     dim3 grid((d.N + 255) / 256, d.B);
     LGM_LAUNCH("k_preproc_bwd", st, (k_preproc_bwd<<<grid, 256, 0, st>>>(d, gaussians, cam_view, cam_view_proj,
                                                                         (const uint2 *)(ws + L.rects),

@@ -544,6 +544,15 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
             vmax = max(vmax, (unsigned)x);
         }
     }
+#ifdef LGM_TIMING_SORT_NOP  // timing-only diagnostic build: the ids stay unsorted (wrong renders)
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_MAXR; r++) {
+        const int e = c0 + r * 64 + lane;
+        if (r < R && e < n) reinterpret_cast<unsigned *>(seg)[e] = (unsigned)pr[r] < n ? (unsigned)seg[0] : 0u;
+    }
+    return;
+#endif
     if (tid == 0) { s_min = 0xffffffffu; s_max = 0u; s_vmax = 0u; s_long = 0; }
     __syncthreads();
     lmin = wave_min_u32(lmin);

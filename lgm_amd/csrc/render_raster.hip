@@ -390,6 +390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         if (tid == 0) {  // per-workgroup timeline (100 MHz s_memrealtime ticks): [8 + 4*tile] start, +1 end
             d.counters[8 + 8 * (size_t)tile] = t_start;
             d.counters[8 + 8 * (size_t)tile + 1] = __builtin_amdgcn_s_memrealtime();
+            d.counters[8 + 8 * (size_t)tile + 7] = c_list;  // list entries staged (walked) by the forward
         }
     }
     if (inside) {

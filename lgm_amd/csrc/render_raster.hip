@@ -66,27 +66,35 @@ constexpr int WU_LD = 68;  // row stride of the per-wave [16 columns][64 pixels]
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 constexpr int MB = 8;      // entries per moment-MFMA batch (columns 0..7: w, 8..15: u)
 
-constexpr int SENT = TILE_PIX;  // sentinel slot: opacity 0, never contributes (pads the per-wave lists)
 // One staged 256-entry chunk, written by LDS DMA (global_load_lds: 16-B lane stride for both the 16-B and the
 // 12-B form): P from gP, Q from gQ, R.xyz from the Gaussian row's colour; R.w holds the Gaussian id (written
 // at commit). Two of these alternate: chunk c+1 streams into one while chunk c is composited from the other.
-struct StageBuf {
-    float4 P[TILE_PIX + 1];  // x, y, A, B
-    float4 Q[TILE_PIX + 1];  // C, opacity, tau, depth
-    float4 R[TILE_PIX + 1];  // r, g, b, id bits
+template <int ROWS>  // entries per chunk; row ROWS is the sentinel
+struct StageBufT {
+    float4 P[ROWS + 1];  // x, y, A, B
+    float4 Q[ROWS + 1];  // C, opacity, tau, depth
+    float4 R[ROWS + 1];  // r, g, b, id bits
 };
-template <int NB, int PAD>  // NB 2: double-buffered (the backward), 1: synchronous staging (the forward)
-struct StageT {                // PAD: list padding = entries evaluated per step (a multiple of 4)
-    StageBuf buf[NB];
-    unsigned char mask[TILE_PIX];          // quadrant mask of the current chunk's entries
-    unsigned short list[4][TILE_PIX + PAD];  // per-wave compacted entry indices, padded with SENT to a multiple of PAD
+using StageBuf = StageBufT<TILE_PIX>;
+template <int NB, int PAD, int ROWS = TILE_PIX>  // NB 2: double-buffered, 1: synchronous staging
+struct StageT {                                   // PAD: list padding = entries evaluated per step (multiple of 4)
+    static constexpr int kRows = ROWS;
+    using Buf = StageBufT<ROWS>;
+    Buf buf[NB];
+    unsigned char mask[ROWS];                 // quadrant mask of the current chunk's entries
+    unsigned short list[4][ROWS + PAD];       // per-wave compacted entry indices, padded with the sentinel (ROWS)
 };
 #ifndef LGM_FWD_DB
 #define LGM_FWD_DB 0  // forward staging: 0 synchronous (measured fastest), 1 always prefetching, 2 from the second chunk
 #endif
 using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 // the backward sits 3 workgroups per CU only just: its LDS must stay <= 53,744 B (measured: 53,776 B ran at 2)
-using StageBwd = StageT<2, 4>;
+#ifndef LGM_BWD_CHUNK
+#define LGM_BWD_CHUNK 128  // backward entries per staged chunk (the per-wave moment slots scale with it)
+#endif
+constexpr int BWD_CHUNK = LGM_BWD_CHUNK;
+static_assert(BWD_CHUNK % 64 == 0 && BWD_CHUNK <= TILE_PIX, "chunk rows");
+using StageBwd = StageT<2, 4, BWD_CHUNK>;
 
 // Wait for every outstanding vector-memory operation of this wave (incl. its LDS DMA). A hard s_waitcnt: the
 // compiler's waitcnt pass sees it, and does not itself track LDS written by DMA.
@@ -117,7 +125,8 @@ __device__ __forceinline__ void lds_dma(const void *src, void *lds_row0) {
 
 // Issue the LDS DMA of one entry (this lane's row of wave w's 64-row slice). Asynchronous: the rows are valid
 // after vm_wait_all() in every issuing wave followed by a barrier.
-__device__ __forceinline__ void stage_dma(StageBuf &B, int w, unsigned gid, size_t gbase, int b, int N,
+template <class Buf>
+__device__ __forceinline__ void stage_dma(Buf &B, int w, unsigned gid, size_t gbase, int b, int N,
                                           const float4 *__restrict__ gP, const float4 *__restrict__ gQ,
                                           const float *__restrict__ gauss) {
     lds_dma<16>(gP + gbase + gid, &B.P[w * 64]);
@@ -128,7 +137,7 @@ __device__ __forceinline__ void stage_dma(StageBuf &B, int w, unsigned gid, size
 // Entry j of a landed chunk: its quadrant mask (the alpha >= 1/255 ellipse against the four 8x8 quadrants) and,
 // for the backward's gradient flush, its Gaussian id.
 template <class Stage>
-__device__ __forceinline__ void stage_commit(Stage &S, StageBuf &B, int j, bool have, unsigned gid, int tx0, int ty0,
+__device__ __forceinline__ void stage_commit(Stage &S, typename Stage::Buf &B, int j, bool have, unsigned gid, int tx0, int ty0,
                                              bool store_id) {
     unsigned char mask = 0;
     if (have) {
@@ -146,38 +155,19 @@ __device__ __forceinline__ void stage_commit(Stage &S, StageBuf &B, int j, bool 
 }
 
 template <class Stage>
-__device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin = 0) {
-    constexpr int PAD = (int)(sizeof(S.list[0]) / sizeof(S.list[0][0])) - TILE_PIX;
+__device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin = 0, int jend = Stage::kRows) {
+    constexpr int PAD = (int)(sizeof(S.list[0]) / sizeof(S.list[0][0])) - Stage::kRows;
     int cnt = 0;
     const unsigned long long lt = lanemask_lt(lane);
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
+    for (int c = 0; c < Stage::kRows / 64; c++) {
         const int j = c * 64 + lane;
-        const bool bit = ((S.mask[j] >> w) & 1u) && j >= jmin;
+        const bool bit = ((S.mask[j] >> w) & 1u) && j >= jmin && j < jend;
         const unsigned long long bal = __ballot(bit);
         if (bit) S.list[w][cnt + __popcll(bal & lt)] = (unsigned short)j;
         cnt += __popcll(bal);
     }
-    if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)SENT;  // pad to the next multiple of PAD
-    return cnt;
-}
-
-// compact_wave restricted to chunk entries j < jend (the backward: positions behind the wave's last contributor
-// touch none of its pixels).
-template <class Stage>
-__device__ __forceinline__ int compact_wave_below(Stage &S, int w, int lane, int jend) {
-    constexpr int PAD = (int)(sizeof(S.list[0]) / sizeof(S.list[0][0])) - TILE_PIX;
-    int cnt = 0;
-    const unsigned long long lt = lanemask_lt(lane);
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-        const int j = c * 64 + lane;
-        const bool bit = ((S.mask[j] >> w) & 1u) && j < jend;
-        const unsigned long long bal = __ballot(bit);
-        if (bit) S.list[w][cnt + __popcll(bal & lt)] = (unsigned short)j;
-        cnt += __popcll(bal);
-    }
-    if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)SENT;  // pad to the next multiple of PAD
+    if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)Stage::kRows;  // pad to the next multiple of PAD
     return cnt;
 }
 
@@ -199,10 +189,10 @@ __device__ __forceinline__ void list_n(const Stage &S, int w, int kk, int (&jj)[
 template <class Stage>
 __device__ __forceinline__ void init_sentinel(Stage &S) {
     if (threadIdx.x < sizeof(S.buf) / sizeof(S.buf[0])) {
-        StageBuf &B = S.buf[threadIdx.x];
-        B.P[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
-        B.Q[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
-        B.R[SENT] = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto &B = S.buf[threadIdx.x];
+        B.P[Stage::kRows] = make_float4(0.f, 0.f, 0.f, 0.f);
+        B.Q[Stage::kRows] = make_float4(0.f, 0.f, 0.f, 0.f);
+        B.R[Stage::kRows] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 
@@ -460,9 +450,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const float *__restrict__ d_depth, const float *__restrict__ d_alpha, const unsigned char *__restrict__ cmask,
     float *__restrict__ accum) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
-    constexpr int LS = TILE_PIX + 1;             // padded LDS row stride (no bank conflicts)
+    constexpr int CH = BWD_CHUNK, LS = CH + 1;  // entries per staged chunk; padded LDS row stride
     __shared__ StageBwd S;
-    __shared__ __attribute__((aligned(16))) float sAcc[LS * NV];  // 9 rows without a depth gradient
+    // per-wave moment slots (plain stores: each wave writes an entry's moments once; no LDS atomics), combined over
+    // the entry's quadrant waves at the chunk's end (then they hold the entry's gradient partials, in wave 0's slot)
+    __shared__ __attribute__((aligned(16))) float sAccW[4][LS * NV];
     __shared__ int sMaxLast;
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
     __shared__ unsigned short sBidx[4][MB];
@@ -541,6 +533,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // MFMA operands: A (features) lane (ql, qk) holds feature ql of wave pixels 32 t + 8 qk + j, j = 0..7
     const int ql = lane & 15, qk = lane >> 4;
     const float cxT = (float)tx0 + 7.5f, cyT = (float)ty0 + 7.5f;
+    // the slot row offset of this lane's result r (row 4 qk + r of column ql), -1 where that result is unused:
+    // w columns keep the geometric moments (rows 0..5), u columns the colour / depth sums (rows 6..8 [9])
+    int mrow[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) {
+        const int row = 4 * qk + rr;
+        const bool live = ql < MB ? row <= 5 : (row >= 6 && row < NV);
+        mrow[rr] = live ? row * LS : -1;
+    }
+    float *myAcc = sAccW[w];
     float *myWU = sWU[w];
     myWU[lane] = dp0;
     myWU[64 + lane] = dp1;
@@ -593,53 +595,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             a2[t2] = cacc;
         }
         const f32x4 acc = a2[0] + a2[1];
-        // D[row = 4 qk + r][col = ql]: moments 0..5 in w columns, rows 6..9 in u columns
-        if (ql < MB) {
-            if (ql < nb) {
-                const int e = sBidx[w][ql];
-                if (qk == 0) {
-                    atomicAdd(&sAcc[0 * LS + e], acc[0]);
-                    atomicAdd(&sAcc[1 * LS + e], acc[1]);
-                    atomicAdd(&sAcc[2 * LS + e], acc[2]);
-                    atomicAdd(&sAcc[3 * LS + e], acc[3]);
-                } else if (qk == 1) {
-                    atomicAdd(&sAcc[4 * LS + e], acc[0]);
-                    atomicAdd(&sAcc[5 * LS + e], acc[1]);
-                }
-            }
-        } else if (ql - MB < nb) {
-            const int e = sBidx[w][ql - MB];
-            if (qk == 1) {
-                atomicAdd(&sAcc[6 * LS + e], acc[2]);
-                atomicAdd(&sAcc[7 * LS + e], acc[3]);
-            } else if (qk == 2) {
-                atomicAdd(&sAcc[8 * LS + e], acc[0]);
-                if (DEPTH) atomicAdd(&sAcc[9 * LS + e], acc[1]);
-            }
+        // D[row = 4 qk + r][col = ql]: moments 0..5 in the w columns, rows 6..9 in the u columns; each lane stores its
+        // (at most 4) live results into this wave's slots at a per-lane row offset fixed for the kernel (mrow)
+        const int e = sBidx[w][ql & (MB - 1)];
+        if ((ql & (MB - 1)) < nb) {
+#pragma unroll
+            for (int rr = 0; rr < 4; rr++)
+                if (mrow[rr] >= 0) myAcc[mrow[rr] + e] = acc[rr];
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     };
 
-    // Staging pipeline (front to back over [s0, s1)): chunk b0 + 256 streams into the other buffer by LDS DMA
+    // Staging pipeline (front to back over [s0, s1)): chunk b0 + CH streams into the other buffer by LDS DMA
     // during chunk b0's compositing and is complete (vm_wait_all) before chunk b0's gradient atomics are issued,
     // so no staging load queues behind them; the sorted ids run one chunk further ahead in a register.
-    unsigned id_cur = s0 + tid < s1 ? ids[s0 + tid] : 0u;
-    if (s0 + tid < s1) stage_dma(S.buf[0], w, id_cur, gbase, b, d.N, gP, gQ, gauss);
-    unsigned id_next = s0 + TILE_PIX + tid < s1 ? ids[s0 + TILE_PIX + tid] : 0u;
+    const bool stager = tid < CH;  // the threads that stage (and test) one chunk row each
+    unsigned id_cur = stager && s0 + tid < s1 ? ids[s0 + tid] : 0u;
+    if (stager && s0 + tid < s1) stage_dma(S.buf[0], w, id_cur, gbase, b, d.N, gP, gQ, gauss);
+    unsigned id_next = stager && s0 + CH + tid < s1 ? ids[s0 + CH + tid] : 0u;
     vm_wait_all();
     int cur = 0;
-    for (int b0 = s0; b0 < s1; b0 += TILE_PIX, cur ^= 1) {
+    for (int b0 = s0; b0 < s1; b0 += CH, cur ^= 1) {
         __syncthreads();
         const int k = b0 + tid;
-        StageBuf &B = S.buf[cur];
-        stage_commit(S, B, tid, k < s1, id_cur, tx0, ty0, true);
-#pragma unroll
-        for (int q = 0; q < NV; q++) sAcc[q * LS + tid] = 0.f;
+        auto &B = S.buf[cur];
+        if (stager) stage_commit(S, B, tid, k < s1, id_cur, tx0, ty0, true);
+        {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
+            float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
+            for (int q = tid; q < 4 * LS * NV / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         __syncthreads();
-        if (k + TILE_PIX < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
+        if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
         id_cur = id_next;
-        id_next = k + 2 * TILE_PIX < s1 ? ids[k + 2 * TILE_PIX] : 0u;
-        const int cnt = compact_wave_below(S, w, lane, wlast - b0);  // positions < wlast only
+        id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
+        const int cnt = compact_wave(S, w, lane, 0, wlast - b0);  // positions < wlast only
         int nb = 0;  // entries in the pending MFMA batch (wave-uniform)
         for (int kk = 0; kk < cnt; kk += BU) {
             int jj4[4];
@@ -704,37 +693,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         }
         if (nb) flush_batch(nb);
         __syncthreads();
-        // moments -> gradient partials, in place (one thread per staged entry)
-        if (b0 + tid < s1) {
+        // moments -> gradient partials (one thread per staged entry): the sum over the four waves' slots,
+        // converted, into wave 0's slots
+        if (tid < CH && b0 + tid < s1) {
             const int j = tid;
             const float4 Pj = B.P[j];
             const float4 Qj = B.Q[j];
             const float xg = Pj.x - cxT, yg = Pj.y - cyT;
             float q[NACC];
 #pragma unroll
-            for (int qq = 0; qq < NV; qq++) q[qq] = sAcc[qq * LS + j];
+            for (int qq = 0; qq < NV; qq++) {
+                float s = 0.f;
+#pragma unroll
+                for (int ww = 0; ww < 4; ww++) s += sAccW[ww][qq * LS + j];
+                q[qq] = s;
+            }
             const float Sx = fmaf(xg, q[0], -q[1]), Sy = fmaf(yg, q[0], -q[2]);
             const float Sxx = fmaf(xg, fmaf(xg, q[0], -2.f * q[1]), q[3]);
             const float Sxy = fmaf(xg, fmaf(yg, q[0], -q[2]), fmaf(-yg, q[1], q[4]));
             const float Syy = fmaf(yg, fmaf(yg, q[0], -2.f * q[2]), q[5]);
-            sAcc[0 * LS + j] = -ddelx_dx * (Pj.z * Sx + Pj.w * Sy);
-            sAcc[1 * LS + j] = -ddely_dy * (Qj.x * Sy + Pj.w * Sx);
-            sAcc[2 * LS + j] = -0.5f * Sxx;
-            sAcc[3 * LS + j] = -0.5f * Sxy;
-            sAcc[4 * LS + j] = -0.5f * Syy;
-            sAcc[5 * LS + j] = Qj.y > 0.f ? q[0] / Qj.y : 0.f;
-            // [6..9] colour / depth sums are already the partials
+            float *o = sAccW[0];
+            o[0 * LS + j] = -ddelx_dx * (Pj.z * Sx + Pj.w * Sy);
+            o[1 * LS + j] = -ddely_dy * (Qj.x * Sy + Pj.w * Sx);
+            o[2 * LS + j] = -0.5f * Sxx;
+            o[3 * LS + j] = -0.5f * Sxy;
+            o[4 * LS + j] = -0.5f * Syy;
+            o[5 * LS + j] = Qj.y > 0.f ? q[0] / Qj.y : 0.f;
+#pragma unroll
+            for (int qq = 6; qq < NV; qq++) o[qq * LS + j] = q[qq];
         }
         vm_wait_all();  // the next chunk's DMA and ids have landed: the atomics below cannot delay them
         __syncthreads();
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
 #pragma unroll
-        for (int it = 0; it < NACC; it++) {
-            const int f = it * TILE_PIX + tid;
+        for (int it = 0; it < CH * NACC / 256; it++) {
+            const int f = it * 256 + tid;
             const int j = f / NACC, q = f - j * NACC;
             if (q < NV && b0 + j < s1) {
-                const float a = sAcc[q * LS + j];
+                const float a = sAccW[0][q * LS + j];
                 if (a != 0.f) atomicAdd(accum + (gbase + reinterpret_cast<const unsigned *>(&B.R[j])[3]) * NACC + q, a);
             }
         }

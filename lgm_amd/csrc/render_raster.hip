@@ -90,7 +90,7 @@ struct StageT {                                   // PAD: list padding = entries
 using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 // the backward sits 3 workgroups per CU only just: its LDS must stay <= 53,744 B (measured: 53,776 B ran at 2)
 #ifndef LGM_BWD_CHUNK
-#define LGM_BWD_CHUNK 128  // backward entries per staged chunk (the per-wave moment slots scale with it)
+#define LGM_BWD_CHUNK 64  // backward entries per staged chunk (the per-wave moment slots scale with it)
 #endif
 constexpr int BWD_CHUNK = LGM_BWD_CHUNK;
 static_assert(BWD_CHUNK % 64 == 0 && BWD_CHUNK <= TILE_PIX, "chunk rows");
@@ -437,7 +437,8 @@ __device__ __forceinline__ float row_sum16(float v) {
 // relative per product). Moments are combined over the tile's four waves in LDS, turned into gradient partials per
 // entry and flushed once per (chunk, entry) to the per-view accumulators.
 #ifndef LGM_BWD_WPE
-#define LGM_BWD_WPE 3  // minimum waves per SIMD the register allocation must allow (4: <= 128 VGPRs)
+#define LGM_BWD_WPE 4  // minimum waves per SIMD the register allocation must allow (4: <= 128 VGPRs; the 64-entry
+                       // chunks' LDS admits 4 workgroups per CU)
 #endif
 template <bool DEPTH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 : LGM_BWD_WPE))) void k_render_bwd(
@@ -619,6 +620,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         __syncthreads();
         const int k = b0 + tid;
         auto &B = S.buf[cur];
+#if LGM_BWD_CHUNK == 64
+        // one row per lane: every wave tests all CH entries against its OWN quadrant (one ellipse test per lane
+        // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
+        if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
+        {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
+            float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
+            for (int q = tid; q < 4 * LS * NV / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        int cnt;
+        {
+            bool hit = false;
+            if (b0 + lane < s1 && lane < wlast - b0) {  // positions < wlast only
+                const float4 p = B.P[lane], q = B.Q[lane];
+                const float qx = (float)(tx0 + ((w & 1) << 3)), qy = (float)(ty0 + ((w >> 1) << 3));
+                hit = ellipse_hits_rect(p.x, p.y, p.z, p.w, q.x, 1.0f / p.z, 1.0f / q.x, q.z, qx, qx + 7.0f, qy,
+                                        qy + 7.0f);
+            }
+            const unsigned long long bal = __ballot(hit);
+            if (hit) S.list[w][__popcll(bal & lanemask_lt(lane))] = (unsigned short)lane;
+            cnt = __popcll(bal);
+            constexpr int PAD = (int)(sizeof(S.list[0]) / sizeof(S.list[0][0])) - CH;
+            if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)CH;
+        }
+        __syncthreads();  // the zeroed slots (and the ids) before any flush
+        if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
+        id_cur = id_next;
+        id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
+#else
         if (stager) stage_commit(S, B, tid, k < s1, id_cur, tx0, ty0, true);
         {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
             float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
@@ -629,6 +658,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         id_cur = id_next;
         id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
         const int cnt = compact_wave(S, w, lane, 0, wlast - b0);  // positions < wlast only
+#endif
         int nb = 0;  // entries in the pending MFMA batch (wave-uniform)
         for (int kk = 0; kk < cnt; kk += BU) {
             int jj4[4];
@@ -727,10 +757,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
 #pragma unroll
-        for (int it = 0; it < CH * NACC / 256; it++) {
+        for (int it = 0; it < (CH * NACC + 255) / 256; it++) {
             const int f = it * 256 + tid;
             const int j = f / NACC, q = f - j * NACC;
-            if (q < NV && b0 + j < s1) {
+            if (q < NV && j < CH && b0 + j < s1) {
                 const float a = sAccW[0][q * LS + j];
                 if (a != 0.f) atomicAdd(accum + (gbase + reinterpret_cast<const unsigned *>(&B.R[j])[3]) * NACC + q, a);
             }

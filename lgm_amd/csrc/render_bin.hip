@@ -280,6 +280,9 @@ __global__ __launch_bounds__(1024) void k_scan(const int *__restrict__ count, in
 // LPT order: the (view, tile) work items sorted by decreasing bucket size (counting sort on n / 8). The
 // compositing kernels take their tiles in this order, so the longest lists start first and the short ones fill
 // the gaps (longest-processing-time-first scheduling). One workgroup of NT threads; hist: ORD_BK ints of LDS.
+#ifndef LGM_SORT_LPT
+#define LGM_SORT_LPT 1  // 1: a separate k_order launch before k_sort, whose workgroups then take tiles in LPT order
+#endif
 constexpr int ORD_THREADS = 1024, ORD_BK = 2048;
 template <int NT>
 __device__ __forceinline__ void order_tiles(int M, long long slot_stride, const int *__restrict__ tile_start,
@@ -677,14 +680,15 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_
                                                      const int *__restrict__ tile_count,
                                                      unsigned long long *__restrict__ pairs, int *__restrict__ order,
                                                      unsigned long long *__restrict__ counters) {
-    if (blockIdx.x == 0) {
+    if (LGM_SORT_LPT == 0 && blockIdx.x == 0) {
         extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
         static_assert(RS_LDS >= (ORD_BK + RS_WAVES) * 4, "order_tiles reuses the sort image");
         int *hist = reinterpret_cast<int *>(smem);
         order_tiles<RS_THREADS>(M, slot_stride, tile_start, tile_count, order, hist, hist + ORD_BK);
         return;
     }
-    const int tile = blockIdx.x - 1;
+    // LGM_SORT_LPT: k_order ran first and the sorts take their tiles longest first too
+    const int tile = LGM_SORT_LPT ? order[blockIdx.x] : (int)blockIdx.x - 1;
     long long base;
     int n;
     tile_range(tile, slot_stride, tile_start, tile_count, base, n);
@@ -737,7 +741,11 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view,
                            cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum)));
             }
-            LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M + 1, RS_THREADS, RS_LDS, st>>>(
+            if (LGM_SORT_LPT) {
+                LGM_LAUNCH("k_order", st, (k_order<<<1, ORD_THREADS, 0, st>>>((int)M, L.slot ? (long long)d.N : -1LL,
+                                                                             tstart, tcount, (int *)(ws + L.order))));
+            }
+            LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M + (LGM_SORT_LPT ? 0 : 1), RS_THREADS, RS_LDS, st>>>(
                                          (int)M, L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs,
                                          (int *)(ws + L.order), d.counters)));
         }

@@ -42,7 +42,10 @@ __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
 #ifndef LGM_BIN_THREADS
 #define LGM_BIN_THREADS 512
 #endif
-constexpr int BIN_THREADS = LGM_BIN_THREADS, BIN_G = BIN_THREADS;
+#ifndef LGM_BIN_ITERS
+#define LGM_BIN_ITERS 3  // measured: 1 -> 50 us, 2 -> 55, 3 -> 46, 4 -> 58 (cfg3)
+#endif
+constexpr int BIN_THREADS = LGM_BIN_THREADS, BIN_G = BIN_THREADS, BIN_ITERS = LGM_BIN_ITERS;
 constexpr int BIN_HITCAP = BIN_THREADS * 6;  // hit-list capacity (typical: ~4 hits per Gaussian)
 static_assert(BIN_THREADS <= 512, "owner index packs into 9 bits");
 
@@ -82,9 +85,6 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     int *hbase = hist + T, *fill = hist + 2 * T;
     int *cur = tile_count + (size_t)bv * T;
     if (tid < 2) s_tot[tid] = 0;
-    if (tid == 0) s_nhit = 0;
-    if (lds)
-        for (int t = tid; t < T; t += BIN_THREADS) hist[t] = 0;
     auto dest = [&](int t, int pos) -> long long {
         return (MODE == EMIT_SLOT ? ((long long)bv * T + t) * slot_stride
                                   : (long long)tile_start[(size_t)bv * T + t]) + pos;
@@ -94,8 +94,14 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                                              8 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x)
                                            : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
+    // BIN_ITERS batches of BIN_G Gaussians per workgroup, one after the other: fewer, longer workgroups fit the
+    // launch into one round of residency (3 workgroups per CU by LDS)
+    for (int it = 0; it < BIN_ITERS; it++) {
+    if (tid == 0) s_nhit = 0;
+    if (lds)
+        for (int t = tid; t < T; t += BIN_THREADS) hist[t] = 0;
     // ---- preprocess, one Gaussian per thread
-    const int i = blockIdx.x * BIN_G + tid;
+    const int i = (blockIdx.x * BIN_ITERS + it) * BIN_G + tid;
     Geo o;
     bool vis = false;
     if (i < d.N) {
@@ -237,6 +243,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         stamp[4] = __builtin_amdgcn_s_memrealtime();
         stamp[5] = (unsigned long long)s_nhit;
     }
+    }  // batches
     if (tid == 0) {
         atomicAdd(&misc[0], s_tot[0]);
         atomicAdd(&misc[1], s_tot[1]);
@@ -722,7 +729,7 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     unsigned long long *pairs = (unsigned long long *)(ws + L.pairs), *misc = (unsigned long long *)(ws + L.misc);
     float *accum = (float *)(ws + L.accum);
     const size_t lds = d.T <= LDS_HIST_MAX ? 3 * (size_t)d.T * 4 : 0;
-    dim3 grid((d.N + BIN_G - 1) / BIN_G, d.BV);
+    dim3 grid((d.N + BIN_G * BIN_ITERS - 1) / (BIN_G * BIN_ITERS), d.BV);
     if (d.N > 0) {
         if (count_only || !L.slot) {
             LGM_LAUNCH("k_bin_count", st, (k_bin<COUNT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,

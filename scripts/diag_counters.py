@@ -44,6 +44,8 @@ res["tile_list_hist_1k"] = np.bincount(nl // 1024).tolist()
 for name, (a, b) in {"fwd": (0, 1), "bwd": (2, 3), "sort": (4, 5)}.items():
     st, en = tl[:, a], tl[:, b]
     ok = en > 0
+    if not ok.any():  # no per-workgroup timeline for this kernel (the backward records none)
+        continue
     st, en = st[ok], en[ok]
     t0 = st.min()
     dur = (en - st) * 0.01  # us
@@ -62,7 +64,7 @@ os.makedirs("gpurun_out", exist_ok=True)
 json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)
 st, en = tl[:, 4], tl[:, 5]
 ok = en > 0
-dur = (en - st) * 0.01
+dur = (en - st) * 0.01 if ok.any() else np.zeros(len(st))
 res2 = {}
 for k in range(int(nl.max()) // 512 + 1):
     m = ok & (nl // 512 == k)

@@ -18,6 +18,12 @@
 #ifndef LGM_FWD_BRANCHY
 #define LGM_FWD_BRANCHY 0  // forward serial chain with per-lane branches (1) or as selects (0)
 #endif
+#ifndef LGM_LIST_PF
+#define LGM_LIST_PF 1  // per-wave list words read one step ahead (forward)
+#endif
+#ifndef LGM_LIST_PF_BWD
+#define LGM_LIST_PF_BWD 1  // the same in the backward
+#endif
 #ifndef LGM_FWD_FU
 #define LGM_FWD_FU 4  // forward entries evaluated per step: 4 or 8
 #endif
@@ -171,19 +177,30 @@ __device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin 
     return cnt;
 }
 
-// U (a multiple of 4) consecutive list entries from kk (a multiple of 4) as wave-uniform (scalar) indices.
+// U (a multiple of 4) consecutive list entries from kk (a multiple of 4): list_raw reads them (an LDS read that can
+// be issued a step ahead), list_decode makes them wave-uniform (scalar) indices, list_n does both.
 template <int U, class Stage>
-__device__ __forceinline__ void list_n(const Stage &S, int w, int kk, int (&jj)[U]) {
+__device__ __forceinline__ void list_raw(const Stage &S, int w, int kk, uint2 (&raw)[U / 4]) {
     static_assert(U % 4 == 0, "list reads are 8-B words");
 #pragma unroll
+    for (int h = 0; h < U / 4; h++) raw[h] = *reinterpret_cast<const uint2 *>(&S.list[w][kk + 4 * h]);
+}
+template <int U>
+__device__ __forceinline__ void list_decode(const uint2 (&raw)[U / 4], int (&jj)[U]) {
+#pragma unroll
     for (int h = 0; h < U / 4; h++) {
-        const uint2 v = *reinterpret_cast<const uint2 *>(&S.list[w][kk + 4 * h]);
-        const unsigned lo = __builtin_amdgcn_readfirstlane(v.x), hi = __builtin_amdgcn_readfirstlane(v.y);
+        const unsigned lo = __builtin_amdgcn_readfirstlane(raw[h].x), hi = __builtin_amdgcn_readfirstlane(raw[h].y);
         jj[4 * h + 0] = lo & 0xffffu;
         jj[4 * h + 1] = lo >> 16;
         jj[4 * h + 2] = hi & 0xffffu;
         jj[4 * h + 3] = hi >> 16;
     }
+}
+template <int U, class Stage>
+__device__ __forceinline__ void list_n(const Stage &S, int w, int kk, int (&jj)[U]) {
+    uint2 raw[U / 4];
+    list_raw<U>(S, w, kk, raw);
+    list_decode<U>(raw, jj);
 }
 
 template <class Stage>
@@ -296,11 +313,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         // FU = 4 entries per step: their alphas are independent of the running transmittance, so they are evaluated
         // together (ILP, branch-free: list padded with the opacity-0 sentinel); only the short T / colour update
         // chain stays serial, in list order, as upstream.
+#if LGM_LIST_PF
+        uint2 lraw[FU / 4];  // the next step's list words, read one step ahead (the list is fixed for the chunk)
+        list_raw<FU>(S, w, 0, lraw);
+#endif
         for (int kk = 0; kk < cnt; kk += FU) {
             if (__ballot(!done) == 0ull) break;
             c_iter += min(FU, cnt - kk);
             int jj[FU];
+#if LGM_LIST_PF
+            list_decode<FU>(lraw, jj);
+#else
             list_n(S, w, kk, jj);
+#endif
             float al[FU];
             float4 cc[FU], Pv[FU], Qv[FU];
             // all the batch's LDS reads first, then one wait: the scheduler would otherwise interleave them with the
@@ -312,6 +337,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
                 const float4 R = B.R[jj[u]];
                 cc[u] = make_float4(R.x, R.y, R.z, 0.f);
             }
+#if LGM_LIST_PF
+            list_raw<FU>(S, w, kk + FU, lraw);  // in bounds: the list rows hold kRows + FU words
+#endif
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < FU; u++) {
@@ -660,9 +688,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         const int cnt = compact_wave(S, w, lane, 0, wlast - b0);  // positions < wlast only
 #endif
         int nb = 0;  // entries in the pending MFMA batch (wave-uniform)
+#if LGM_LIST_PF_BWD
+        static_assert(BU == 4, "the list prefetch reads whole 4-entry words");
+        uint2 lraw[1];  // the next step's list word, read one step ahead
+        list_raw<4>(S, w, 0, lraw);
+#endif
         for (int kk = 0; kk < cnt; kk += BU) {
             int jj4[4];
+#if LGM_LIST_PF_BWD
+            list_decode<4>(lraw, jj4);
+#else
             list_n(S, w, kk & ~3, jj4);
+#endif
             int jj[BU];
 #pragma unroll
             for (int u = 0; u < BU; u++) jj[u] = jj4[(kk & 3) + u];
@@ -675,6 +712,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 const float4 Rj = B.R[jj[u]];
                 cc[u] = make_float4(Rj.x, Rj.y, Rj.z, 0.f);
             }
+#if LGM_LIST_PF_BWD
+            list_raw<4>(S, w, kk + 4, lraw);  // in bounds: the list rows hold kRows + 4 words
+#endif
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < BU; u++) {

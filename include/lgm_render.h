@@ -87,6 +87,10 @@ int lgm_render_debug_counters(unsigned long long *device_counters);
  * the workspace; the backward passes d_image only where 0 <= unclamped <= 1 (torch's clamp gradient), so no
  * separate clamp kernels or unclamped copy are needed. */
 #define LGM_RENDER_CLAMP_IMAGE 2
+/* LGM_RENDER_BACKWARD_AGAIN (lgm_render_backward only): this workspace's forward has already been through a
+ * backward (autograd with retain_graph): its gradient accumulators are cleared first. The forward's binning
+ * zeroes them, so a first backward needs no clearing pass. */
+#define LGM_RENDER_BACKWARD_AGAIN 4
 
 /* Option flags (process-wide, default 0). LGM_RENDER_NO_CULL bins upstream's full 3-sigma tile rects instead of
  * dropping (Gaussian, tile) pairs where alpha < 1/255 is provable for every pixel; outputs are identical either

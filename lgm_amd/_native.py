@@ -45,6 +45,7 @@ _lib = None
 
 ABI_VERSION = 2
 RENDER_CLAMP_IMAGE = 2  # include/lgm_render.h LGM_RENDER_CLAMP_IMAGE
+RENDER_BACKWARD_AGAIN = 4  # include/lgm_render.h LGM_RENDER_BACKWARD_AGAIN
 
 
 class NativeError(RuntimeError):

@@ -21,12 +21,20 @@ namespace {
 
 enum BinMode { COUNT = 0, EMIT_SLOT = 1, EMIT_PACKED = 2 };
 
-__device__ __forceinline__ int wave_incl_scan(int x, int lane) {
-#pragma unroll
-    for (int dd = 1; dd < 64; dd <<= 1) {
-        const int y = __shfl_up(x, dd, 64);
-        if (lane >= dd) x += y;
-    }
+// Inclusive wavefront scans on the DPP network (row shifts inside each 16-lane row, then the row_bcast:15 /
+// row_bcast:31 carries across rows): VALU only, no LDS permute round trips. A lane whose DPP source does not
+// exist takes `old` (the operation's identity).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ int dpp_src(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, 0xf, false);
+}
+__device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
+    x += dpp_src<0x111>(0, x);       // row_shr:1
+    x += dpp_src<0x112>(0, x);       // row_shr:2
+    x += dpp_src<0x114>(0, x);       // row_shr:4
+    x += dpp_src<0x118>(0, x);       // row_shr:8
+    x += dpp_src<0x142, 0xa>(0, x);  // row_bcast:15 into rows 1, 3
+    x += dpp_src<0x143, 0xc>(0, x);  // row_bcast:31 into rows 2, 3
     return x;
 }
 
@@ -56,12 +64,14 @@ struct BinRec {  // one Gaussian's emit record in LDS (48 B)
     unsigned long long key;
 };
 
-__device__ __forceinline__ int wave_incl_max(int v, int lane) {
-#pragma unroll
-    for (int dd = 1; dd < 64; dd <<= 1) {
-        const int y = __shfl_up(v, dd, 64);
-        if (lane >= dd) v = max(v, y);
-    }
+__device__ __forceinline__ int wave_incl_max(int v, int /*lane*/) {
+    constexpr int LO = -2147483647 - 1;
+    v = max(v, dpp_src<0x111>(LO, v));
+    v = max(v, dpp_src<0x112>(LO, v));
+    v = max(v, dpp_src<0x114>(LO, v));
+    v = max(v, dpp_src<0x118>(LO, v));
+    v = max(v, dpp_src<0x142, 0xa>(LO, v));
+    v = max(v, dpp_src<0x143, 0xc>(LO, v));
     return v;
 }
 
@@ -145,7 +155,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     if (lane == 0 && nref) atomicAdd(&s_tot[1], nref);
     // ---- flattened exact tile tests of the wavefront's candidates
     const int incl = wave_incl_scan(nc, lane), excl = incl - nc;
-    const int total = __shfl(incl, 63, 64);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
     sExcl[tid] = excl;
     __syncthreads();  // histogram zeroed; records and exclusive offsets visible
     if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
@@ -160,7 +170,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         int v = sHead[tid];
         if (lane == 0 && v < 0) v = carry;
         v = wave_incl_max(v, lane);
-        carry = __shfl(v, 63, 64);
+        carry = __builtin_amdgcn_readlane(v, 63);
         const int c = base0 + lane;
         bool hit = false;
         int t = 0, owner = 0;
@@ -184,7 +194,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         if (lds) {
             int slot0 = 0;
             if (MODE != COUNT && lane == 0) slot0 = atomicAdd(&s_nhit, __popcll(hm));
-            slot0 = __shfl(slot0, 0, 64);
+            slot0 = __builtin_amdgcn_readlane(slot0, 0);
             if (hit) {
                 const int rk = atomicAdd(&hist[t], 1);
                 if (MODE != COUNT) {

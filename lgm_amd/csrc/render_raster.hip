@@ -840,11 +840,10 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         float2 *acc2 = reinterpret_cast<float2 *>(accum + k * NACC);
         float acc[NACC];
 #pragma unroll
-        for (int q = 0; q < NACC / 2; q++) {  // read, then re-zero for the next backward over this workspace
+        for (int q = 0; q < NACC / 2; q++) {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
             const float2 a = acc2[q];
             acc[2 * q] = a.x;
             acc[2 * q + 1] = a.y;
-            acc2[q] = make_float2(0.f, 0.f);
         }
         const float dm2x = acc[0], dm2y = acc[1];
         const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
@@ -961,6 +960,13 @@ int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, fl
 int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_view, const float *cam_view_proj,
                       const float *bg, const float *d_image, const float *d_depth, const float *d_alpha,
                       float *d_gaussians, float *d_means2D, char *ws, const Layout &L, hipStream_t st) {
+    // the per-view accumulators were zeroed by the forward's binning; a repeated backward of the same forward
+    // clears what the previous one left
+    if ((d.options & LGM_RENDER_BACKWARD_AGAIN) &&
+        hipMemsetAsync(ws + L.accum, 0, (size_t)d.BV * d.N * NACC * sizeof(float), st) != hipSuccess) {
+        set_error("hipMemsetAsync failed");
+        return LGM_E_HIP;
+    }
     auto bwd = d_depth ? k_render_bwd<true> : k_render_bwd<false>;
     // work items: chunk 0 of every tile, then one per checkpoint slot (unused slots exit at once)
     LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(d.BV * d.T + 8 * L.ck_region), 256, 0, st>>>(

@@ -62,6 +62,7 @@ class _RasterizeBatched(torch.autograd.Function):
         ctx.set_materialize_grads(False)  # unused outputs (LGM never uses depth) arrive as None, not zeros
         ctx.ws, ctx.ws_bytes, ctx.cap = ws, ws_bytes, cap
         ctx.params = (tanx, tany, scale_modifier, H, W, options)
+        ctx.backwards = 0  # a repeated backward (retain_graph) must clear the previous one's accumulators
         return image, depth, alpha
 
     @staticmethod
@@ -77,11 +78,13 @@ class _RasterizeBatched(torch.autograd.Function):
         d_alpha = None if d_alpha is None else d_alpha.float().contiguous()
         d_g = torch.empty_like(g)
         L = _native.lib()
+        bwd_options = options | (_native.RENDER_BACKWARD_AGAIN if ctx.backwards else 0)
+        ctx.backwards += 1
         _native.check(L.lgm_render_backward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
                                             _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
                                             _native.ptr(d_image), _native.ptr(d_depth), _native.ptr(d_alpha),
                                             _native.ptr(d_g), None, _native.ptr(ctx.ws), ctx.ws_bytes, ctx.cap,
-                                            options, _native.stream_of(g.device)), "lgm_render_backward")
+                                            bwd_options, _native.stream_of(g.device)), "lgm_render_backward")
         return d_g, None, None, None, None, None, None, None, None, None
 
 

@@ -123,6 +123,22 @@ def test_forward_deterministic(cuda):
         assert np.array_equal(a[k], b[k]), k
 
 
+def test_repeated_backward_retain_graph(cuda):
+    """A second backward of one forward (retain_graph) gives the first one's gradient: the forward's binning zeroes
+    the accumulators, and the repeat clears what the first backward left (LGM_RENDER_BACKWARD_AGAIN)."""
+    g, cv, cvp = scene(N=3000, V=2, seed=5)
+    gd = g.to(cuda).requires_grad_(True)
+    img, _, alp = rasterize(gd, cv.to(cuda), cvp.to(cuda), torch.ones(3, device=cuda), TAN, TAN, 64, 64)
+    w = torch.randn(img.shape, generator=torch.Generator().manual_seed(3)).to(cuda)
+    loss = (img * w).sum() + alp.sum()
+    (first,) = torch.autograd.grad(loss, gd, retain_graph=True)
+    (second,) = torch.autograd.grad(loss, gd)
+    torch.cuda.synchronize()
+    assert first.abs().sum().item() > 0
+    # the same sums in a different atomic order: equal to fp32 rounding
+    assert rel_l2(second.cpu().numpy(), first.cpu().numpy()) < 1e-5
+
+
 def test_cfg2_full_size_forward(cuda, oracle_mod):
     # BASELINE config 2: 50k Gaussians, 1 camera, 256^2, fwd only (seed 0)
     g, cv, cvp = scene(N=50000, V=1, seed=0)

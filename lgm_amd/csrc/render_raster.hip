@@ -612,10 +612,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
             bf16x8 bh, bl;
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const __bf16 h = (__bf16)xs[j];
-                bh[j] = h;
-                bl[j] = (__bf16)(xs[j] - (float)h);
+            for (int j = 0; j < 8; j++) {  // hi = the top 16 bits (exact), lo = the rest rounded: ~2^-17 relative
+                const unsigned ub = __builtin_bit_cast(unsigned, xs[j]);
+                bh[j] = __builtin_bit_cast(__bf16, (unsigned short)(ub >> 16));
+                bl[j] = (__bf16)(xs[j] - __builtin_bit_cast(float, ub & 0xffff0000u));
             }
             f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);

@@ -24,6 +24,9 @@
 #ifndef LGM_LIST_PF_BWD
 #define LGM_LIST_PF_BWD 1  // the same in the backward
 #endif
+#ifndef LGM_BWD_MASKSEL
+#define LGM_BWD_MASKSEL 1
+#endif
 #ifndef LGM_FWD_FU
 #define LGM_FWD_FU 4  // forward entries evaluated per step: 4 or 8
 #endif
@@ -744,7 +747,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 const float inv = fmaf(fmaf(-om, r0, 1.0f), r0, r0);  // 1 / (1 - alpha), ~0.5 ulp
                 const float dL_dalpha = fmaf(Tr, cdp, -(DK - Dup) * inv);
                 Tr = Tr - aT;
+#if LGM_BWD_MASKSEL
+                // a bit mask, not a select: the compiler would otherwise sink the 1/(1 - alpha) chain into an
+                // exec-masked branch that almost never skips
+                const unsigned keep = alpha != 0.f ? 0xffffffffu : 0u;
+                v[u][0] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, Gw[u] * dL_dalpha) & keep);
+#else
                 v[u][0] = alpha != 0.f ? Gw[u] * dL_dalpha : 0.f;
+#endif
                 v[u][1] = aT;  // dchannel_dcolor (0 for a skipped entry)
             }
 #pragma unroll

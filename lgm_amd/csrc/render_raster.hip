@@ -486,10 +486,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     __shared__ StageBwd S;
     // per-wave moment slots (plain stores: each wave writes an entry's moments once; no LDS atomics), combined over
     // the entry's quadrant waves at the chunk's end (then they hold the entry's gradient partials, in wave 0's slot)
-    __shared__ __attribute__((aligned(16))) float sAccW[4][LS * NV];
+    // (row NV of each wave's slot is a junk row: the MFMA results a lane does not keep are stored there, so the
+    // stores need no exec-masked branches)
+    __shared__ __attribute__((aligned(16))) float sAccW[4][LS * (NV + 1)];
     __shared__ int sMaxLast;
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
-    __shared__ unsigned short sBidx[4][MB];
     // ---- work item: (tile, chunk c, checkpoint slot)
     const int M = d.BV * d.T;
     int tile, c = 0, slot = -1;
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     for (int rr = 0; rr < 4; rr++) {
         const int row = 4 * qk + rr;
         const bool live = ql < MB ? row <= 5 : (row >= 6 && row < NV);
-        mrow[rr] = live ? row * LS : -1;
+        mrow[rr] = live ? row * LS : -1;  // -1: stored to the junk row
     }
     float *myAcc = sAccW[w];
     float *myWU = sWU[w];
@@ -604,6 +605,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    int myj = 0;  // the chunk row of this lane's batch column (ql & 7)
     auto flush_batch = [&](int nb) {
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         // B operand: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t), split hi + lo
@@ -629,12 +631,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         const f32x4 acc = a2[0] + a2[1];
         // D[row = 4 qk + r][col = ql]: moments 0..5 in the w columns, rows 6..9 in the u columns; each lane stores its
         // (at most 4) live results into this wave's slots at a per-lane row offset fixed for the kernel (mrow)
-        const int e = sBidx[w][ql & (MB - 1)];
-        if ((ql & (MB - 1)) < nb) {
+        const bool col_ok = (ql & (MB - 1)) < nb;
 #pragma unroll
-            for (int rr = 0; rr < 4; rr++)
-                if (mrow[rr] >= 0) myAcc[mrow[rr] + e] = acc[rr];
-        }
+        for (int rr = 0; rr < 4; rr++) myAcc[(col_ok && mrow[rr] >= 0) ? mrow[rr] + myj : NV * LS + lane] = acc[rr];
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     };
 
@@ -656,8 +655,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
         if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
         {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
+            static_assert((4 * LS * (NV + 1)) % 4 == 0, "slot zeroing by float4");
             float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
-            for (int q = tid; q < 4 * LS * NV / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q = tid; q < 4 * LS * (NV + 1) / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         int cnt;
         {
@@ -681,8 +681,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #else
         if (stager) stage_commit(S, B, tid, k < s1, id_cur, tx0, ty0, true);
         {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
+            static_assert((4 * LS * (NV + 1)) % 4 == 0, "slot zeroing by float4");
             float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
-            for (int q = tid; q < 4 * LS * NV / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q = tid; q < 4 * LS * (NV + 1) / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         __syncthreads();
         if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
@@ -764,7 +765,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 if (bal == 0ull) continue;
                 myWU[nb * WU_LD + lane] = v[u][0];         // w
                 myWU[(MB + nb) * WU_LD + lane] = v[u][1];  // u
-                if (lane == 0) sBidx[w][nb] = (unsigned short)jj[u];
+                myj = (lane & (MB - 1)) == nb ? jj[u] : myj;  // the entry of batch column nb (w and u columns)
                 if (++nb == MB) {
                     flush_batch(MB);
                     nb = 0;

@@ -73,11 +73,11 @@ int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussian
  * [2] backward wavefront-entry iterations, [3] backward (pixel, Gaussian) gradient contributions,
  * [4] dense / [5] sparse wavefront reductions, [6] tile-list entries staged by the forward, [7] max forward
  * iterations of one wavefront; then 8 entries per tile t (B*V*T tiles): s_memrealtime stamps (100 MHz)
- * [8+8t] fwd start, [+1] fwd end, [+2] bwd start (after the early exit test), [+3] bwd end, [+4] sort start,
+ * [8+8t] fwd start, [+1] fwd end, [+2], [+3] unused (the backward keeps per-work-item records), [+4] sort start,
  * [+5] sort end, and [+6] the tile's binned list length; then 8 entries per binning workgroup
  * (B*V*ceil(N/512)): phase stamps [0] start, [1] preprocessed, [2] tile tests done, [3] reserved, [4] end,
- * and [5] its binned pairs; then 4 entries per backward work item: start/end stamps, (length | first entry << 20
- * | tile << 40) and wavefront iterations -- so the buffer must hold 8 + 8*B*V*tiles + 8*B*V*ceil(N/512) +
+ * and [5] its binned pairs; then 4 entries per backward work item: start/end stamps, (entries | chunk << 20 |
+ * tile << 40) and one unused -- so the buffer must hold 8 + 8*B*V*tiles + 8*B*V*ceil(N/512) +
  * 4*5*B*V*tiles entries.
  * NULL disables (default). Process-wide; not for concurrent use. */
 int lgm_render_debug_counters(unsigned long long *device_counters);

@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const float *__restrict__ ck, const int2 *__restrict__ cklist, const int *__restrict__ nck,
     const unsigned *__restrict__ ckctr, int ck_region, const float *__restrict__ d_img,
     const float *__restrict__ d_depth, const float *__restrict__ d_alpha, const unsigned char *__restrict__ cmask,
-    float *__restrict__ accum) {
+    float *__restrict__ accum, long long item_stamps) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
     constexpr int CH = BWD_CHUNK, LS = CH + 1;  // entries per staged chunk; padded LDS row stride
     __shared__ StageBwd S;
@@ -556,6 +556,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const int s0 = c * TILE_PIX;
     if (s0 >= nlist) return;  // workgroup-uniform
     const int s1 = (c + 1 <= nck[tile]) ? min(nlist, s0 + TILE_PIX) : nlist;
+    const unsigned long long t_item = d.counters ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const float bg_dot = bg[0] * dp0 + bg[1] * dp1 + bg[2] * dp2;
     float cdpf = fmaf(cf.x, dp0, fmaf(cf.y, dp1, cf.z * dp2));
     if (DEPTH) cdpf = fmaf(cf.w, dpd, cdpf);
@@ -817,6 +818,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             }
         }
     }
+    if (d.counters && tid == 0) {  // work-item timeline (lgm_render_debug_counters): start, end, (length | chunk | tile)
+        unsigned long long *o = d.counters + item_stamps + 4 * (size_t)blockIdx.x;
+        o[0] = t_item;
+        o[1] = __builtin_amdgcn_s_memrealtime();
+        o[2] = (unsigned long long)(s1 - s0) | ((unsigned long long)c << 20) | ((unsigned long long)tile << 40);
+    }
 }
 
 // k_preproc_bwd: grid (ceil(N/256), B), block 256. Sums over the scene's views in order (deterministic).
@@ -988,7 +995,9 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
                                        (const float4 *)(ws + L.cfin), (const float *)(ws + L.ck),
                                        (const int2 *)(ws + L.cklist), (const int *)(ws + L.nck),
                                        (const unsigned *)(ws + L.misc) + 4, L.ck_region, d_image, d_depth, d_alpha,
-                                       (const unsigned char *)(ws + L.cmask), (float *)(ws + L.accum))));
+                                       (const unsigned char *)(ws + L.cmask), (float *)(ws + L.accum),
+                                       // (debug counters: after the per-tile and per-binning-workgroup records)
+                                       8 + 8LL * d.BV * d.T + 8LL * d.BV * ((d.N + 511) / 512))));
     dim3 grid((d.N + 255) / 256, d.B);
     LGM_LAUNCH("k_preproc_bwd", st, (k_preproc_bwd<<<grid, 256, 0, st>>>(d, gaussians, cam_view, cam_view_proj,
                                                                         (const uint2 *)(ws + L.rects),

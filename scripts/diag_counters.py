@@ -16,7 +16,7 @@ g = synthetic_gaussians(1, 100000, seed=1).to(dev).requires_grad_(True)
 cv, cvp, cp = orbit_cameras(6)
 d_img, _, d_alpha, bg = synthetic_upstream_grads(1, 6, 256, 256, seed=1001)
 M = 6 * 256
-NB = 6 * ((100000 + 1535) // 1536)  # k_bin workgroups (3 batches of 512 Gaussians each)
+NB = 6 * ((100000 + 511) // 512)  # binning records reserved (k_bin uses the first 6 * ceil(N / 1536))
 NI = 5 * M  # backward work-item capacity
 cnt = torch.zeros(8 + 8 * M + 8 * NB + 4 * NI, dtype=torch.int64, device=dev)
 L = _native.lib()

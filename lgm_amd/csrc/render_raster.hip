@@ -27,6 +27,9 @@
 #ifndef LGM_BWD_MASKSEL
 #define LGM_BWD_MASKSEL 1
 #endif
+#ifndef LGM_BWD_AOP_SELECT
+#define LGM_BWD_AOP_SELECT 1
+#endif
 #ifndef LGM_FWD_FU
 #define LGM_FWD_FU 4  // forward entries evaluated per step: 4 or 8
 #endif
@@ -592,6 +595,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             int lx2, ly2;
             tile_pixel(w * 64 + p, lx2, ly2);
             const float fx = (float)(tx0 + lx2) - cxT, fy = (float)(ty0 + ly2) - cyT;
+#if LGM_BWD_AOP_SELECT
+            // selects, not a per-lane if-chain (whose exec-masked branches every work item's prologue paid)
+            const float dpv = myWU[min(max(ql - 6, 0), 3) * 64 + p];
+            const float f = ql == 0   ? 1.f
+                            : ql == 1 ? fx
+                            : ql == 2 ? fy
+                            : ql == 3 ? fx * fx
+                            : ql == 4 ? fx * fy
+                            : ql == 5 ? fy * fy
+                            : ql <= 9 ? dpv
+                                      : 0.f;
+#else
             float f = 0.f;
             if (ql == 0) f = 1.f;
             else if (ql == 1) f = fx;
@@ -600,6 +615,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             else if (ql == 4) f = fx * fy;
             else if (ql == 5) f = fy * fy;
             else if (ql <= 9) f = myWU[(ql - 6) * 64 + p];
+#endif
             const __bf16 h = (__bf16)f;
             Ah[t2][j] = h;
             Al[t2][j] = (__bf16)(f - (float)h);

@@ -1,21 +1,30 @@
-"""bench.py -- BASELINE.json metric: Mpixels/s of forward+backward Gaussian rasterization, 256^2, 100k Gaussians,
-6 views (BASELINE config 3), on 1/2/4/8 MI355X.
+"""bench.py -- BASELINE.json metric: Mpixels/s of forward+backward Gaussian rasterization (256^2, 100k Gaussians,
+6 views; BASELINE config 3 scenes) on 1/2/4/8 MI355X.
 
-A step = GaussianRenderer.render (core/gs.py:31-98 API: forward of all 6 views, clamp) + autograd backward to
-dL/dgaussians [1,N,14] for fixed seeded upstream gradients. Weak scaling: every rank renders its OWN scene
-(seed 1 + rank; scene-sharded, no data-path collective); value = total pixels of all ranks / max
-rank time. Per-kernel durations come from HIP events recorded by liblgm_amd on the launch stream inside the timed
-region (lgm_amd._native.KernelProfiler); `roofline` prices the dominant kernel with SURVEY.md §8(d)'s algorithmic
-bytes. The CPU baseline (rank 0, N=1) is the oracle port (oracle/raster_oracle.c, OpenMP over views) on the same
-scene for a bounded number of repetitions.
+Workload (SURVEY.md §8(d) "scaling"): a fixed pool of 8 cfg3 scenes x 6 views (48 renders of 100k Gaussians at
+256^2, seed 2), sharded by scene over the G ranks (8/G scenes per GPU, rendered by ONE batched call per rank;
+no data-path collective) -> strong scaling. A step = GaussianRenderer.render (core/gs.py:31-98 API, clamp
+in-kernel) of the rank's scenes + autograd backward to dL/dgaussians for fixed seeded upstream gradients of image
+and alpha (LGM's loss inputs, core/models.py:141-153). value = all pixels of the pool / max-over-ranks time.
+
+Secondary objects on the same line:
+  * "cfg3_view_sharded": ONE cfg3 scene (seed 1) whose 6 views are split over the G ranks, plus the RCCL SUM
+    all-reduce of dL/dgaussians [1,N,14]; at G = 1 this is exactly BASELINE config 3;
+  * "cfg2": 50k Gaussians x 1 view x 256^2 forward only (BASELINE config 2), rank 0;
+  * "attention": LGM's heaviest MVAttention level, bf16 fwd+bwd, MFMA and exp rooflines;
+  * "roofline": the dominant kernel priced with SURVEY §8(d)'s algorithmic bytes over its HIP-event time;
+  * "cpu_baseline": the CPU oracle port on all host cores (rank 0, N = 1).
 
     python bench.py [--gpus N --steps K --warmup W]
+With --gpus N > 1 and no torchrun environment, bench.py spawns the N ranks itself (before any GPU call).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,42 +33,72 @@ sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
-N_GAUSS, VIEWS, RES = 100_000, 6, 256
+# v_exp_f32: 8 issue cycles per 64-lane wave instruction per SIMD (MI355X_MICROARCH.md constants table):
+# 256 CUs x 4 SIMDs x 8 lanes/cycle x 2.4 GHz
+PEAK_EXP_PER_S = 256 * 4 * 8 * 2.4e9
+N_GAUSS, VIEWS, RES, POOL_SCENES = 100_000, 6, 256, 8
+POOL_SEED, CFG3_SEED, CFG2_SEED = 2, 1, 0
 
 
-def kernel_bytes(N, V, K, P):
-    """SURVEY.md §8(d) algorithmic bytes per launch (all V views of one scene): fwd = 56N + 60K + 20P,
-    bwd = 112N + 84K + 28P per view, K = upstream's num_rendered (summed over views here) even though fewer pairs
-    are binned after exact culling (a build that culls more is still credited with K_ref).
-    k_bin (preprocess + emit) carries 56N + 8K per view, k_sort 8K."""
+def kernel_bytes(N, BV, K, P):
+    """SURVEY.md §8(d) algorithmic bytes per launch over BV renders: fwd = 56N + 60K + 20P, bwd = 112N + 84K + 28P
+    per view, K = upstream's num_rendered summed over the views (a build that culls more is still credited with
+    K_ref). k_bin (preprocess + emit) carries 56N + 8K per view, k_sort 8K."""
     return {
-        "k_bin": 56 * N * V + 8 * K,
+        "k_bin": 56 * N * BV + 8 * K,
         "k_sort": 8 * K,
-        "k_render_fwd": 44 * K + 20 * P * V,
-        "k_render_bwd": 84 * K + 28 * P * V,
-        "k_preproc_bwd": 112 * N * V,
+        "k_render_fwd": 44 * K + 20 * P * BV,
+        "k_render_bwd": 84 * K + 28 * P * BV,
+        "k_preproc_bwd": 112 * N * BV,
     }
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC profile of this workload (rocprofv3 FETCH_SIZE x 2 +
-    WRITE_SIZE, gfx950-corrected, scripts/gpu_pmc.sh -> scripts/pmc_summary.py --json), or null."""
+def pmc_record(kernel):
+    """HBM bytes per launch of `kernel` and its limiter counters from the committed PMC profile of this workload
+    (rocprofv3 passes, gfx950-corrected: scripts/gpu_pmc.sh -> scripts/pmc_summary.py --json), or nulls."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         d = json.load(open(path))
         rec = d[kernel]
-        return {"traffic": int(rec["hbm_read_bytes"] + rec["hbm_write_bytes"]),
-                "traffic_source": f"profiles/pmc_latest.json (PMC passes at commit {d['_meta'].get('commit', '?')})"}
-    except (OSError, KeyError, ValueError):
+        out = {"traffic": int(rec["hbm_read_bytes"] + rec["hbm_write_bytes"]),
+               "traffic_source": f"profiles/pmc_latest.json ({d['_meta'].get('workload', '?')}, "
+                                 f"commit {d['_meta'].get('commit', '?')})"}
+        lim = {k: rec[k] for k in ("wait_frac", "valu_busy_frac", "lds_bank_conflict_frac") if k in rec}
+        if lim:
+            out["counters"] = lim
+        return out
+    except (OSError, KeyError, ValueError, TypeError):
         return {"traffic": None}
 
 
+def host_cpu():
+    model = "?"
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = min(usable, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else usable
+    return model, os.cpu_count() or 1, share
+
+
 def cpu_baseline(g, cv, cvp, tan, bg, d_img, d_alpha, seconds):
+    """The oracle port (oracle/raster_oracle.c) fwd+bwd of the cfg3 scene on the host's CPU share: OpenMP over the
+    6 views x threads over each view's tiles (nested), a bounded number of repetitions."""
     from oracle import oracle as O
     O.build()
-    threads = min(os.cpu_count() or 1, VIEWS)
+    model, ncpu, share = host_cpu()
+    views = min(VIEWS, share)
+    tiles = max(1, share // views)
     args = (g.numpy(), cv.numpy(), cvp.numpy(), tan, RES, RES, bg.numpy())
-    kw = dict(d_image=d_img.numpy(), d_alpha=d_alpha.numpy(), nthreads=threads)
+    kw = dict(d_image=d_img.numpy(), d_alpha=d_alpha.numpy(), nthreads=views, tile_threads=tiles)
     O.render(*args, **kw)  # warm
     reps, t0 = 0, time.perf_counter()
     while True:
@@ -68,16 +107,17 @@ def cpu_baseline(g, cv, cvp, tan, bg, d_img, d_alpha, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": round(reps * VIEWS * RES * RES / el / 1e6, 3), "unit": "Mpixels/s", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle/raster_oracle.c fwd+bwd of the rank-0 cfg3 scene (100k Gaussians x 6 views x 256^2), "
-                      f"{reps} repetitions in {el:.1f} s, OpenMP over views"}
+    return {"value": round(reps * VIEWS * RES * RES / el / 1e6, 3), "unit": "Mpixels/s", "cores": views * tiles,
+            "kind": "port", "host_cpu": model, "host_cpus_visible": ncpu, "host_cpu_share": share,
+            "sample": f"oracle/raster_oracle.c fwd+bwd of the cfg3 scene (seed 1: 100k Gaussians x 6 views x 256^2),"
+                      f" {reps} repetitions in {el:.1f} s, {views} threads over views x {tiles} over tiles"}
 
 
 def attention_bench(dev, steps: int = 10):
-    """Secondary object: LGM's heaviest MVAttention level (core/unet.py:35-49 at C=512, 32x32, 4 views -> L = 4096
-    tokens, 16 heads, D = 32; 8 objects per GPU as in the 'big' training batch), bf16 fwd+bwd through the HIP
-    kernels (lgm_amd/attention.py), with torch's SDPA on the same tensors as a comparator. FLOPs 14 B H L^2 D."""
+    """LGM's heaviest MVAttention level (core/unet.py:35-49 at C=512, 32x32, 4 views -> L = 4096 tokens, 16 heads,
+    D = 32; 8 objects per GPU as in the 'big' training batch), bf16 fwd+bwd through the HIP kernels, torch SDPA on
+    the same tensors as a comparator. FLOPs 14 B H L^2 D; exps 3 B H L^2 (forward + the two backward kernels each
+    recompute P from the LSE)."""
     import torch
     import torch.nn.functional as F
 
@@ -123,25 +163,45 @@ def attention_bench(dev, steps: int = 10):
     except RuntimeError:
         ms_sdpa = None
     flops = 14.0 * B * H * L * L * D
+    exps = 3.0 * B * H * L * L
     tf = flops / ms / 1e9
     return {"workload": "MVAttention C=512 32x32 x 4 views (L=4096, 16 heads, D=32), 8 objects, fwd+bwd",
             "dtype": "bf16", "ms_per_step": round(ms, 4), "tflops": round(tf, 1),
             "roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / PEAK_BF16_TFLOPS, 4)},
+            "exp_roofline": {"achieved_Gexp_s": round(exps / ms / 1e6, 1), "peak_Gexp_s": PEAK_EXP_PER_S / 1e9,
+                             "frac": round(exps / (ms / 1e3) / PEAK_EXP_PER_S, 4),
+                             "note": "at D=32 one exp per 128 MFMA FLOP: the v_exp_f32 issue rate bounds the "
+                                     "softmax as tightly as the MFMA peak bounds the contractions"},
             "kernels": {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in kern.items()},
             "torch_sdpa_tflops": round(flops / ms_sdpa / 1e9, 1) if ms_sdpa else None}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-attention", action="store_true", help="skip the secondary attention measurement")
-    args = ap.parse_args()
+def cfg2_bench(dev, steps):
+    """BASELINE config 2: 50k Gaussians, 1 camera, 256^2, RGB+alpha forward only (bg = ones, seed 0)."""
+    import torch
 
+    from lgm_amd import GaussianRenderer, Options
+    from lgm_amd.cameras import orbit_cameras
+    from lgm_amd.synthetic import synthetic_gaussians
+    r = GaussianRenderer(Options(output_size=RES))
+    g = synthetic_gaussians(1, 50_000, seed=CFG2_SEED).to(dev)
+    cv, cvp, cp = (t[None].to(dev) for t in orbit_cameras(1))
+    bg = torch.ones(3, device=dev)
+    with torch.no_grad():
+        for _ in range(5):
+            r.render(g, cv, cvp, cp, bg_color=bg)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r.render(g, cv, cvp, cp, bg_color=bg)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    return {"workload": "cfg2: 50k Gaussians x 1 view x 256^2, forward only", "ms_per_step": round(1e3 * el / steps, 4),
+            "Mpixels_per_s": round(steps * RES * RES / el / 1e6, 2)}
+
+
+def run(args):
     import torch
 
     from lgm_amd import dist as D
@@ -156,26 +216,33 @@ def main():
     from lgm_amd.gs import count_pairs
     from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads
 
-    seed = D.scene_seed(rank)
-    g_cpu = synthetic_gaussians(1, N_GAUSS, seed=seed)
-    cv, cvp, cp = orbit_cameras(VIEWS)
-    d_img, _, d_alpha, bg = synthetic_upstream_grads(1, VIEWS, RES, RES, seed=seed + 1000)
     renderer = GaussianRenderer(Options(output_size=RES))
-    g = g_cpu.to(dev).requires_grad_(True)
-    cvd, cvpd, cpd = cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev)
-    bgd, d_imgd, d_alphad = bg.to(dev), d_img.to(dev), d_alpha.to(dev)
     tan = float(renderer.tan_half_fov)
-    K_binned, K = count_pairs(g.detach(), cvd, cvpd, tan, tan, RES, RES)
+    cv, cvp, cp = orbit_cameras(VIEWS)
+
+    # ---- the scaling pool: scenes s0..s1 of 8 on this rank, one batched render
+    s0, s1 = D.shard_range(POOL_SCENES, rank, world)
+    B = s1 - s0
+    pool = synthetic_gaussians(POOL_SCENES, N_GAUSS, seed=POOL_SEED)
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(POOL_SCENES, VIEWS, RES, RES, seed=POOL_SEED + 1000)
+    g = pool[s0:s1].contiguous().to(dev).requires_grad_(True)
+    cvd = cv[None].expand(B, -1, -1, -1).contiguous().to(dev)
+    cvpd = cvp[None].expand(B, -1, -1, -1).contiguous().to(dev)
+    cpd = cp[None].expand(B, -1, -1).contiguous().to(dev)
+    bgd = bg.to(dev)
+    d_imgd, d_alphad = d_img[s0:s1].contiguous().to(dev), d_alpha[s0:s1].contiguous().to(dev)
+    K_binned, K = count_pairs(g.detach(), cvd, cvpd, tan, tan, RES, RES) if B else (0, 0)
 
     def step():
+        if B == 0:
+            return
         out = renderer.render(g, cvd, cvpd, cpd, bg_color=bgd)
         torch.autograd.backward([out["image"], out["alpha"]], [d_imgd, d_alphad])
         g.grad = None
 
     for _ in range(args.warmup):
         step()
-    # the timed steps run with nothing attached; per-kernel HIP-event times come from a second, untimed pass of
-    # the same K steps (the event records add marker packets between launches)
+    # timed steps with nothing attached; per-kernel HIP-event times from a second, untimed pass of the same steps
     el = D.timed_steps(step, args.steps, info, torch.cuda.synchronize, dev)
     prof = _native.KernelProfiler()
     with prof:
@@ -186,14 +253,10 @@ def main():
     prof.close()
 
     P = RES * RES
-    pixels = world * VIEWS * P * args.steps
+    pixels = POOL_SCENES * VIEWS * P * args.steps
     value = pixels / el / 1e6
-    kb = kernel_bytes(N_GAUSS, VIEWS, K, P)
+    kb = kernel_bytes(N_GAUSS, B * VIEWS, K, P)
     per_kernel = {k: {"avg_us": round(1e3 * ms / n, 2), "launches": n} for k, (n, ms) in kern.items()}
-    dom = max(kern.items(), key=lambda kv: kv[1][1])[0]
-    dom_avg_s = kern[dom][1] / kern[dom][0] / 1e3
-    achieved = kb.get(dom, 0) / dom_avg_s / 1e9
-    step_bytes = sum(kb.values())
     ms_step = 1e3 * el / args.steps
     result = {
         "metric": "Mpixels/s fwd+bwd Gaussian raster (256^2, 100k gauss, 6 views)",
@@ -204,29 +267,119 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (SURVEY.md 8(d): raw~N(0,1) through LGM activations, 6 orbit cameras r=1.5 fovy 49.1, "
-                "seeded upstream grads); one scene per GPU",
-        "config": {"workload": "cfg3: 100k Gaussians x 6 views x 256^2, render fwd+bwd (GaussianRenderer API)",
-                   "gaussians": N_GAUSS, "views": VIEWS, "H": RES, "W": RES, "scenes_per_gpu": 1,
-                   "pairs_K_reference": K, "pairs_binned": K_binned, "parallelism": f"scene-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS,
-                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "bytes_per_launch": kb.get(dom, 0),
-                     **pmc_traffic(dom)},
-        "step_roofline": {"bytes": step_bytes, "achieved_GBs": round(step_bytes / (ms_step / 1e3) / 1e9, 2),
-                          "frac": round(step_bytes / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4)},
+                "seeded upstream grads of image and alpha); scaling pool seed 2",
+        "config": {"workload": f"scaling pool: {POOL_SCENES} cfg3 scenes (100k Gaussians x 6 views x 256^2 each), "
+                               f"render fwd+bwd (GaussianRenderer API), sharded by scene: {B} scene(s) on rank 0",
+                   "gaussians": N_GAUSS, "views": VIEWS, "H": RES, "W": RES, "pool_scenes": POOL_SCENES,
+                   "scenes_per_gpu": B, "global_batch": POOL_SCENES, "pairs_K_reference_rank0": K,
+                   "pairs_binned_rank0": K_binned, "parallelism": f"scene-sharded x{world} (no collective)"},
         "kernels": per_kernel,
     }
-    if not args.no_attention:
-        result["attention"] = attention_bench(dev)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(g_cpu, cv[None], cvp[None], tan, bg, d_img, d_alpha,
-                                              args.cpu_seconds)
+    if kern:
+        dom = max(kern.items(), key=lambda kv: kv[1][1])[0]
+        dom_avg_s = kern[dom][1] / kern[dom][0] / 1e3
+        achieved = kb.get(dom, 0) / dom_avg_s / 1e9
+        binned = kernel_bytes(N_GAUSS, B * VIEWS, K_binned, P).get(dom, 0) / dom_avg_s / 1e9
+        step_bytes = sum(kb.values())
+        result["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS,
+                              "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                              "bytes_per_launch": kb.get(dom, 0),
+                              "frac_at_binned_K": round(binned / PEAK_HBM_GBS, 4),
+                              "limiter": "latency / LDS issue, not HBM (see DESIGN.md §4: PMC wait, VALU and LDS "
+                                         "bank-conflict fractions)",
+                              **pmc_record(dom)}
+        result["step_roofline"] = {"bytes": step_bytes, "achieved_GBs": round(step_bytes / (ms_step / 1e3) / 1e9, 2),
+                                   "frac": round(step_bytes / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}
+
+    # ---- cfg3 with its views split over the ranks + one RCCL all-reduce of dL/dgaussians
+    v0, v1 = D.shard_range(VIEWS, rank, world)
+    g3 = synthetic_gaussians(1, N_GAUSS, seed=CFG3_SEED).to(dev).requires_grad_(True)
+    d3_img, _, d3_alpha, bg3 = synthetic_upstream_grads(1, VIEWS, RES, RES, seed=CFG3_SEED + 1000)
+    c3v, c3p, c3c = cv[None, v0:v1].contiguous().to(dev), cvp[None, v0:v1].contiguous().to(dev), cp[None, v0:v1].to(dev)
+    d3i, d3a, bg3d = d3_img[:, v0:v1].contiguous().to(dev), d3_alpha[:, v0:v1].contiguous().to(dev), bg3.to(dev)
+    ar = {"ms": 0.0}
+
+    def step3():
+        if v1 > v0:
+            out = renderer.render(g3, c3v, c3p, c3c, bg_color=bg3d)
+            torch.autograd.backward([out["image"], out["alpha"]], [d3i, d3a])
+            grad = g3.grad
+        else:
+            grad = torch.zeros_like(g3)
+        D.allreduce_scene_grads(grad, info)
+        g3.grad = None
+
+    for _ in range(args.warmup):
+        step3()
+    el3 = D.timed_steps(step3, args.steps, info, torch.cuda.synchronize, dev)
+    if world > 1:  # the all-reduce on its own, same tensor size
+        buf = torch.zeros(1, N_GAUSS, 14, device=dev)
+        for _ in range(3):
+            D.allreduce_scene_grads(buf, info)
+        ar["ms"] = 1e3 * D.timed_steps(lambda: D.allreduce_scene_grads(buf, info), args.steps, info,
+                                       torch.cuda.synchronize, dev) / args.steps
+    result["cfg3_view_sharded"] = {
+        "workload": "cfg3 (BASELINE config 3): ONE scene, 100k Gaussians x 6 views x 256^2, fwd+bwd; views split "
+                    f"over {world} rank(s) + SUM all-reduce of dL/dgaussians [1,N,14] fp32 (RCCL)",
+        "ms_per_step": round(1e3 * el3 / args.steps, 4),
+        "Mpixels_per_s": round(VIEWS * P * args.steps / el3 / 1e6, 2),
+        "allreduce_ms": round(ar["ms"], 4) if world > 1 else None}
+
     if rank == 0:
+        result["cfg2"] = cfg2_bench(dev, args.steps)
+        if not args.no_attention:
+            result["attention"] = attention_bench(dev)
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(g3.detach().cpu(), cv[None], cvp[None], tan, bg3, d3_img, d3_alpha,
+                                                  args.cpu_seconds)
         print(json.dumps(result), flush=True)
     D.finalize(info)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawned(local_rank, world, port, argv):
+    """Child rank of a self-launched multi-GPU run: torchrun's environment, then the ordinary entry point."""
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse(argv))
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-attention", action="store_true", help="skip the secondary attention measurement")
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if "RANK" in os.environ:
+        if args.gpus != world_env:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_env} from the launcher")
+        run(args)
+    elif args.gpus > 1:
+        # no launcher: start the ranks here, before anything touches the GPU (children, not an exec)
+        import torch.multiprocessing as mp
+        mp.start_processes(_spawned, args=(args.gpus, _free_port(), sys.argv[1:]), nprocs=args.gpus,
+                           start_method="spawn")
+    else:
+        run(args)
 
 
 if __name__ == "__main__":

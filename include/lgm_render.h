@@ -16,7 +16,7 @@
  *   cam_view       [B,V,4,4] the transposed w2c exactly as core/gs.py:54 passes it (read column-major)
  *   cam_view_proj  [B,V,4,4] likewise (core/gs.py:55)
  *   bg             [3]
- *   image          [B,V,3,H,W] UNCLAMPED (core/gs.py:87's clamp is applied by the caller, as the reference does)
+ *   image          [B,V,3,H,W] unclamped, or clamp(0, 1) as core/gs.py:87 when options has LGM_RENDER_CLAMP_IMAGE
  *   depth, alpha   [B,V,1,H,W]
  * Error behaviour: every entry point returns 0 on success and a negative LGM_E* code on failure; it never
  * throws across the ABI. lgm_last_error() returns a thread-local description of the last failure.
@@ -67,6 +67,20 @@ int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussian
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
                         float *d_gaussians, float *d_means2D, void *workspace, size_t workspace_bytes,
                         long long pair_capacity, int options, void *stream);
+
+/* Inspection of the state a forward left in its workspace (the equivalent of upstream's saved binningBuffer /
+ * imgBuffer: point_list + ranges, n_contrib, accum_alpha), for parity tests and debugging. Stream-ordered.
+ * lgm_render_tile_lists: tile_counts_out (DEVICE int32 [B*V*T], T = ceil(W/16)*ceil(H/16), tile-major per view)
+ * receives each (view, tile)'s list length; if ids_out is not NULL, the tile's Gaussian ids in compositing
+ * (depth, then id) order are copied to ids_out[offsets[bv*T + t] ...] (offsets: DEVICE int64 [B*V*T], e.g. the
+ * exclusive cumsum of the counts). Replaces reading point_list[ranges[t].x .. ranges[t].y) of the EXT.
+ * lgm_render_pixel_state: per-pixel n_contrib (1 + list position of the last accepted entry) and final
+ * transmittance, [B,V,H,W] each (DEVICE; either may be NULL). */
+int lgm_render_tile_lists(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
+                          long long pair_capacity, int *tile_counts_out, const long long *offsets,
+                          unsigned *ids_out, void *stream);
+int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
+                           long long pair_capacity, int *n_contrib_out, float *final_T_out, void *stream);
 
 /* Diagnostics: while device_counters (a DEVICE uint64[8], caller-zeroed) is set, the render kernels add work
  * counts to it: [0] forward wavefront-entry iterations, [1] accepted (pixel, Gaussian) contributions,

@@ -31,6 +31,9 @@ SIGNATURES = {
     "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _c_ll, _vp, _c_size, _vp]),
     "lgm_attn_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "lgm_render_tile_lists": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp,
+                                       _vp]),
+    "lgm_render_pixel_state": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp]),
     "lgm_render_debug_counters": (_c_int, [_vp]),
     "lgm_render_set_flags": (_c_int, [_c_int]),
     "lgm_profiler_create": (_vp, []),

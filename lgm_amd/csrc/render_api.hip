@@ -43,6 +43,43 @@ int check_common(int B, int V, int N, int H, int W, const void *g, const void *c
 
 bool capacity_ok(long long cap) { return cap <= 0x7fffffffLL; }
 
+// Inspection kernels (lgm_render_tile_lists / lgm_render_pixel_state): plain copies out of the workspace.
+__global__ __launch_bounds__(256) void k_tile_counts(int M, long long slot_stride, const int *__restrict__ tile_start,
+                                                     const int *__restrict__ tile_count, int *__restrict__ out) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= M) return;
+    long long base;
+    int n;
+    lgm::tile_range(t, slot_stride, tile_start, tile_count, base, n);
+    out[t] = n;
+}
+// one workgroup per (view, tile): its sorted ids (u32, in place at the start of its pair range) -> ids_out
+__global__ __launch_bounds__(256) void k_tile_ids(long long slot_stride, const int *__restrict__ tile_start,
+                                                  const int *__restrict__ tile_count,
+                                                  const unsigned long long *__restrict__ pairs,
+                                                  const long long *__restrict__ offsets, unsigned *__restrict__ ids_out) {
+    const int t = blockIdx.x;
+    long long base;
+    int n;
+    lgm::tile_range(t, slot_stride, tile_start, tile_count, base, n);
+    const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base);
+    unsigned *dst = ids_out + offsets[t];
+    for (int e = threadIdx.x; e < n; e += 256) dst[e] = ids[e];
+}
+
+int check_ws(int B, int V, int N, int H, int W, const void *ws, size_t ws_bytes, long long cap, lgm::Layout &L) {
+    if (B <= 0 || V <= 0 || N < 0 || H <= 0 || W <= 0) {
+        lgm::set_error("invalid sizes (B=%d V=%d N=%d H=%d W=%d)", B, V, N, H, W);
+        return LGM_E_INVALID;
+    }
+    L = lgm::make_layout(B, V, N, H, W, cap);
+    if (!ws || ws_bytes < L.total) {
+        lgm::set_error("workspace too small (%zu < %zu)", ws_bytes, L.total);
+        return LGM_E_WORKSPACE;
+    }
+    return LGM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -96,8 +133,8 @@ int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians
         return LGM_E_INVALID;
     }
     const lgm::Layout L = lgm::make_layout(B, V, N, H, W, pair_capacity);
-    if (!capacity_ok(L.cap)) {
-        lgm::set_error("pair capacity %lld exceeds 2^31; use lgm_render_count_pairs + an exact capacity", L.cap);
+    if (!L.slot && !capacity_ok(L.cap)) {  // packed tile offsets are int32; slot offsets are 64-bit
+        lgm::set_error("pair capacity %lld exceeds 2^31", L.cap);
         return LGM_E_INVALID;
     }
     if (!workspace || workspace_bytes < L.total) {
@@ -110,6 +147,49 @@ int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians
     rc = lgm::launch_binning(d, gaussians, cam_view, cam_view_proj, ws, L, radii_out, stats_out, false, st);
     if (rc) return rc;
     return lgm::launch_render_fwd(d, gaussians, bg, image, depth, alpha, ws, L, st);
+}
+
+int lgm_render_tile_lists(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
+                          long long pair_capacity, int *tile_counts_out, const long long *offsets,
+                          unsigned *ids_out, void *stream) {
+    lgm::clear_error();
+    lgm::Layout L;
+    int rc = check_ws(B, V, N, H, W, workspace, workspace_bytes, pair_capacity, L);
+    if (rc) return rc;
+    if (!tile_counts_out || (ids_out && !offsets)) {
+        lgm::set_error("null tile_counts_out / offsets");
+        return LGM_E_INVALID;
+    }
+    const int T = ((W + lgm::BX - 1) / lgm::BX) * ((H + lgm::BY - 1) / lgm::BY), M = B * V * T;
+    const char *ws = (const char *)workspace;
+    const long long stride = L.slot ? (long long)N : -1LL;
+    const int *ts = (const int *)(ws + L.tile_start), *tc = (const int *)(ws + L.tile_count);
+    hipStream_t st = (hipStream_t)stream;
+    LGM_LAUNCH("k_tile_counts", st, (k_tile_counts<<<(M + 255) / 256, 256, 0, st>>>(M, stride, ts, tc, tile_counts_out)));
+    if (ids_out && N > 0)
+        LGM_LAUNCH("k_tile_ids", st, (k_tile_ids<<<M, 256, 0, st>>>(stride, ts, tc,
+                                     (const unsigned long long *)(ws + L.pairs), offsets, ids_out)));
+    return LGM_OK;
+}
+
+int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
+                           long long pair_capacity, int *n_contrib_out, float *final_T_out, void *stream) {
+    lgm::clear_error();
+    lgm::Layout L;
+    int rc = check_ws(B, V, N, H, W, workspace, workspace_bytes, pair_capacity, L);
+    if (rc) return rc;
+    const size_t P = (size_t)B * V * H * W;
+    const char *ws = (const char *)workspace;
+    hipStream_t st = (hipStream_t)stream;
+    if (n_contrib_out && hipMemcpyAsync(n_contrib_out, ws + L.n_contrib, P * 4, hipMemcpyDeviceToDevice, st) != hipSuccess) {
+        lgm::set_error("hipMemcpyAsync failed");
+        return LGM_E_HIP;
+    }
+    if (final_T_out && hipMemcpyAsync(final_T_out, ws + L.final_T, P * 4, hipMemcpyDeviceToDevice, st) != hipSuccess) {
+        lgm::set_error("hipMemcpyAsync failed");
+        return LGM_E_HIP;
+    }
+    return LGM_OK;
 }
 
 int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,

@@ -72,12 +72,19 @@ struct Dims {
 
 // ------------------------------------------------------------------------------------------------------------
 // Camera helpers: the 4x4 matrices are the row-major torch tensors of core/gs.py:54-55 read column-major.
+//
+// Every helper of the forward preprocess runs with FP contraction OFF and in the oracle's operation order
+// (oracle/raster_oracle.c: glm-order matrix products, left-to-right sums): the integer results derived from it
+// -- radii, tile rects, (Gaussian, tile) pair counts and the depth sort keys -- are then bit-identical to the
+// restatement (tests/test_render_parity_gpu.py), not merely close.
 __device__ __forceinline__ void xf43(const float *M, float x, float y, float z, float o[3]) {
+#pragma clang fp contract(off)
     o[0] = M[0] * x + M[4] * y + M[8] * z + M[12];
     o[1] = M[1] * x + M[5] * y + M[9] * z + M[13];
     o[2] = M[2] * x + M[6] * y + M[10] * z + M[14];
 }
 __device__ __forceinline__ void xf44(const float *M, float x, float y, float z, float o[4]) {
+#pragma clang fp contract(off)
     o[0] = M[0] * x + M[4] * y + M[8] * z + M[12];
     o[1] = M[1] * x + M[5] * y + M[9] * z + M[13];
     o[2] = M[2] * x + M[6] * y + M[10] * z + M[14];
@@ -86,16 +93,23 @@ __device__ __forceinline__ void xf44(const float *M, float x, float y, float z, 
 
 // glm-convention rotation matrix R[col][row] from the un-normalised quaternion (r,x,y,z) (upstream semantics).
 __device__ __forceinline__ void quat_rot(const float q[4], float R[3][3]) {
+#pragma clang fp contract(off)
     const float r = q[0], x = q[1], y = q[2], z = q[3];
     R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - r * z); R[0][2] = 2.f * (x * z + r * y);
     R[1][0] = 2.f * (x * y + r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - r * x);
     R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
 }
 
-// Sigma = M^T M with M = S*R (glm): Sigma[c][r] = sum_k s_k^2 R[c][k] R[r][k]; stored (00,01,02,11,12,22).
+// Sigma = M^T M with M = S*R (glm): M[c][k] = s_k R[c][k], Sigma[c][r] = sum_k M[r][k] M[c][k] (the oracle's
+// m3_mul order); stored (00,01,02,11,12,22).
 __device__ __forceinline__ void cov3d(const float s[3], const float R[3][3], float c3[6]) {
-    const float s0 = s[0] * s[0], s1 = s[1] * s[1], s2 = s[2] * s[2];
-#define LGM_SIG(c, r) (s0 * R[c][0] * R[r][0] + s1 * R[c][1] * R[r][1] + s2 * R[c][2] * R[r][2])
+#pragma clang fp contract(off)
+    float M[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) M[c][k] = s[k] * R[c][k];
+#define LGM_SIG(c, r) (M[r][0] * M[c][0] + M[r][1] * M[c][1] + M[r][2] * M[c][2])
     c3[0] = LGM_SIG(0, 0); c3[1] = LGM_SIG(0, 1); c3[2] = LGM_SIG(0, 2);
     c3[3] = LGM_SIG(1, 1); c3[4] = LGM_SIG(1, 2); c3[5] = LGM_SIG(2, 2);
 #undef LGM_SIG
@@ -109,6 +123,7 @@ struct ProjCtx {
 };
 __device__ __forceinline__ ProjCtx make_proj(const float *Vw, float mx, float my, float mz, float fx, float fy,
                                              float tanx, float tany) {
+#pragma clang fp contract(off)
     ProjCtx P;
     xf43(Vw, mx, my, mz, P.t);
     const float limx = 1.3f * tanx, limy = 1.3f * tany;
@@ -127,7 +142,10 @@ __device__ __forceinline__ ProjCtx make_proj(const float *Vw, float mx, float my
     }
     return P;
 }
+// cov = T^T Sigma^T T (glm order, as the oracle's cov2d): with s0 = Sigma T0 and s1 = Sigma T1 (T0, T1 the
+// non-zero columns of T), a = T0 . s0, b = T0 . s1, c = T1 . s1, each summed left to right.
 __device__ __forceinline__ void cov2d(const ProjCtx &P, const float c3[6], float &a, float &b, float &c) {
+#pragma clang fp contract(off)
     const float S[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
     float s0[3], s1[3];
 #pragma unroll
@@ -136,7 +154,7 @@ __device__ __forceinline__ void cov2d(const ProjCtx &P, const float c3[6], float
         s1[k] = S[k][0] * P.T1[0] + S[k][1] * P.T1[1] + S[k][2] * P.T1[2];
     }
     a = P.T0[0] * s0[0] + P.T0[1] * s0[1] + P.T0[2] * s0[2] + 0.3f;
-    b = P.T1[0] * s0[0] + P.T1[1] * s0[1] + P.T1[2] * s0[2];
+    b = s1[0] * P.T0[0] + s1[1] * P.T0[1] + s1[2] * P.T0[2];
     c = P.T1[0] * s1[0] + P.T1[1] * s1[1] + P.T1[2] * s1[2] + 0.3f;
 }
 
@@ -186,6 +204,7 @@ struct Geo {
 // can reach q <= tau. tau is inflated (below) so fp32 rounding of q can never re-admit a culled pixel.
 __device__ __forceinline__ bool preprocess_one(const float *g, const float *Vw, const float *Pm, const Dims &d,
                                                Geo &o) {
+#pragma clang fp contract(off)
     float hom[4], pv[3];
     xf44(Pm, g[0], g[1], g[2], hom);
     const float pw = 1.0f / (hom[3] + 0.0000001f);

@@ -17,8 +17,21 @@ import torch
 from . import _native
 from .ply import read_ply, write_ply
 
-# Sync-free worst-case workspace when it fits this many bytes; otherwise count pairs exactly (one host sync).
-_WS_BUDGET = int(float(os.environ.get("LGM_AMD_WS_BUDGET_GB", "8")) * (1 << 30))
+# Slot-mode (sync-free, worst-case B*V*T*N pair slots) workspace when it fits this many bytes; otherwise the pairs
+# are counted exactly first (one host sync per batch -- the reference syncs once per VIEW for num_rendered).
+# Default: a quarter of the device's HBM (72 GB of an MI355X's 288: cfg3 needs 1.2 GB, the 8-scene pool 9.8 GB,
+# LGM 'big' with 20 views at 512^2 25 GB). LGM_AMD_WS_BUDGET_GB overrides.
+_WS_BUDGET = int(float(os.environ["LGM_AMD_WS_BUDGET_GB"]) * (1 << 30)) if "LGM_AMD_WS_BUDGET_GB" in os.environ \
+    else None
+_dev_mem = {}
+
+
+def _ws_budget(dev) -> int:
+    if _WS_BUDGET is not None:
+        return _WS_BUDGET
+    if dev not in _dev_mem:
+        _dev_mem[dev] = torch.cuda.get_device_properties(dev).total_memory
+    return _dev_mem[dev] // 4
 
 
 def _tiles(H: int, W: int) -> int:
@@ -35,10 +48,9 @@ class _RasterizeBatched(torch.autograd.Function):
         V = cam_view.shape[1]
         dev = g.device
         stream = _native.stream_of(dev)
-        worst = B * V * N * _tiles(H, W)
         cap = 0
         ws_bytes = L.lgm_render_workspace_size(B, V, N, H, W, 0)
-        if ws_bytes > _WS_BUDGET or worst >= 2 ** 31:
+        if ws_bytes > _ws_budget(dev):
             # exact pair count (the reference syncs once per view for this; we sync once per batch)
             small = L.lgm_render_workspace_size(B, V, N, H, W, 1)
             ws = torch.empty(small, dtype=torch.uint8, device=dev)
@@ -58,16 +70,18 @@ class _RasterizeBatched(torch.autograd.Function):
                                            _native.ptr(image), _native.ptr(depth), _native.ptr(alpha), None,
                                            _native.ptr(ws), ws_bytes, cap, None, options, stream),
                       "lgm_render_forward")
-        ctx.save_for_backward(g, cam_view, cam_view_proj, bg)
+        # the workspace is saved like an input: autograd frees it after a (non-retain_graph) backward, so a training
+        # loop that keeps the previous step's outputs alive does not hold two workspaces
+        ctx.save_for_backward(g, cam_view, cam_view_proj, bg, ws)
         ctx.set_materialize_grads(False)  # unused outputs (LGM never uses depth) arrive as None, not zeros
-        ctx.ws, ctx.ws_bytes, ctx.cap = ws, ws_bytes, cap
+        ctx.ws_bytes, ctx.cap = ws_bytes, cap
         ctx.params = (tanx, tany, scale_modifier, H, W, options)
         ctx.backwards = 0  # a repeated backward (retain_graph) must clear the previous one's accumulators
         return image, depth, alpha
 
     @staticmethod
     def backward(ctx, d_image, d_depth, d_alpha):
-        g, cam_view, cam_view_proj, bg = ctx.saved_tensors
+        g, cam_view, cam_view_proj, bg, ws = ctx.saved_tensors
         tanx, tany, scale_modifier, H, W, options = ctx.params
         B, N = g.shape[0], g.shape[1]
         V = cam_view.shape[1]
@@ -83,7 +97,7 @@ class _RasterizeBatched(torch.autograd.Function):
         _native.check(L.lgm_render_backward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
                                             _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
                                             _native.ptr(d_image), _native.ptr(d_depth), _native.ptr(d_alpha),
-                                            _native.ptr(d_g), None, _native.ptr(ctx.ws), ctx.ws_bytes, ctx.cap,
+                                            _native.ptr(d_g), None, _native.ptr(ws), ctx.ws_bytes, ctx.cap,
                                             bwd_options, _native.stream_of(g.device)), "lgm_render_backward")
         return d_g, None, None, None, None, None, None, None, None, None
 
@@ -123,6 +137,58 @@ def count_pairs(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scal
                                            small, _native.ptr(k), _native.stream_of(dev)), "lgm_render_count_pairs")
     kk = k.tolist()
     return int(kk[0]), int(kk[1])
+
+
+def forward_state(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scale_modifier=1.0, lists=False):
+    """Runs one forward and returns what it left in its workspace (numpy, one host sync), for parity tests and
+    debugging -- the equivalent of reading upstream's saved buffers (radii, point_list/ranges, n_contrib):
+      radii [B,V,N] int32; K_binned / K_reference (as count_pairs); tile_counts [B,V,T] int32;
+      n_contrib, final_T [B,V,H,W]; with lists=True, ids[b][v] = the view's tile lists concatenated (tile-major,
+      each in compositing order)."""
+    L = _native.lib()
+    g = gaussians.float().contiguous()
+    dev = g.device
+    B, N, V = g.shape[0], g.shape[1], cam_view.shape[1]
+    cv = cam_view.to(dev, torch.float32).contiguous()
+    cvp = cam_view_proj.to(dev, torch.float32).contiguous()
+    stream = _native.stream_of(dev)
+    ws_bytes = L.lgm_render_workspace_size(B, V, N, H, W, 0)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    bg = torch.zeros(3, device=dev)
+    image = torch.empty(B, V, 3, H, W, device=dev)
+    depth = torch.empty(B, V, 1, H, W, device=dev)
+    alpha = torch.empty(B, V, 1, H, W, device=dev)
+    radii = torch.empty(B, V, N, dtype=torch.int32, device=dev)
+    stats = torch.zeros(2, dtype=torch.int64, device=dev)
+    _native.check(L.lgm_render_forward(B, V, N, H, W, _native.ptr(g), _native.ptr(cv), _native.ptr(cvp),
+                                       _native.ptr(bg), float(tanfovx), float(tanfovy), float(scale_modifier),
+                                       _native.ptr(image), _native.ptr(depth), _native.ptr(alpha), _native.ptr(radii),
+                                       _native.ptr(ws), ws_bytes, 0, _native.ptr(stats), 0, stream),
+                  "lgm_render_forward")
+    T = _tiles(H, W)
+    counts = torch.empty(B * V * T, dtype=torch.int32, device=dev)
+    _native.check(L.lgm_render_tile_lists(B, V, N, H, W, _native.ptr(ws), ws_bytes, 0, _native.ptr(counts), None,
+                                          None, stream), "lgm_render_tile_lists")
+    n_contrib = torch.empty(B, V, H, W, dtype=torch.int32, device=dev)
+    final_T = torch.empty(B, V, H, W, dtype=torch.float32, device=dev)
+    _native.check(L.lgm_render_pixel_state(B, V, N, H, W, _native.ptr(ws), ws_bytes, 0, _native.ptr(n_contrib),
+                                           _native.ptr(final_T), stream), "lgm_render_pixel_state")
+    out = {"radii": radii.cpu().numpy(), "tile_counts": counts.view(B, V, T).cpu().numpy(),
+           "n_contrib": n_contrib.cpu().numpy(), "final_T": final_T.cpu().numpy()}
+    k = stats.tolist()
+    out["K_binned"], out["K_reference"] = int(k[0]), int(k[1])
+    if lists:
+        c64 = counts.to(torch.int64)
+        offsets = (torch.cumsum(c64, 0) - c64).contiguous()
+        total = int(c64.sum().item())
+        ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        _native.check(L.lgm_render_tile_lists(B, V, N, H, W, _native.ptr(ws), ws_bytes, 0, _native.ptr(counts),
+                                              _native.ptr(offsets), _native.ptr(ids), stream), "lgm_render_tile_lists")
+        flat = ids[:total].cpu().numpy()
+        per_view = c64.view(B * V, T).sum(1).tolist()
+        bounds = np.concatenate([[0], np.cumsum(per_view)])
+        out["ids"] = [[flat[bounds[b * V + v]:bounds[b * V + v + 1]] for v in range(V)] for b in range(B)]
+    return out
 
 
 class GaussianRenderer:

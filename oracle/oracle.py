@@ -50,6 +50,11 @@ def lib(f64: bool = False):
         L.lgm_oracle_tile_lists.restype = ctypes.c_longlong
         L.lgm_oracle_tile_lists.argtypes = [ctypes.c_int, f32p, f32p, f32p, rp, rp,
                                             rp, ctypes.c_int, ctypes.c_int, i32p, i32p, ctypes.c_longlong]
+        L.lgm_oracle_forward_state.restype = ctypes.c_longlong
+        L.lgm_oracle_forward_state.argtypes = [ctypes.c_int, f32p, f32p, f32p, rp, rp, rp, ctypes.c_int,
+                                               ctypes.c_int, i32p, f32p]
+        L.lgm_oracle_set_tile_threads.restype = None
+        L.lgm_oracle_set_tile_threads.argtypes = [ctypes.c_int]
         _libs[f64] = L
     return _libs[f64]
 
@@ -63,8 +68,10 @@ def _c(a, dtype=np.float32):
 
 
 def render(gaussians, cam_view, cam_view_proj, tanfov: float, H: int, W: int, bg, scale_modifier: float = 1.0,
-           d_image=None, d_depth=None, d_alpha=None, nthreads: int = 0, f64: bool = False):
-    """Forward (+ optional backward) of B x V renders.
+           d_image=None, d_depth=None, d_alpha=None, nthreads: int = 0, f64: bool = False, tile_threads: int = 1):
+    """Forward (+ optional backward) of B x V renders. nthreads: OpenMP threads over the B x V views;
+    tile_threads > 1 instead runs the views in sequence with that many threads over each view's tiles (the CPU
+    baseline on all host cores; backward sums in a different order, equal to double rounding).
 
     gaussians [B,N,14]; cam_view/cam_view_proj [B,V,4,4] (row-major torch layout, as core/gs.py passes them);
     bg [3]. Returns dict with image [B,V,3,H,W] (unclamped), depth/alpha [B,V,1,H,W], K (total pairs),
@@ -90,10 +97,12 @@ def render(gaussians, cam_view, cam_view_proj, tanfov: float, H: int, W: int, bg
     if nthreads <= 0:
         nthreads = min(os.cpu_count() or 1, B * V)
     fp = (lambda a: None if a is None else a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))) if f64 else _f
+    lib(f64).lgm_oracle_set_tile_threads(int(tile_threads))
     rc = lib(f64).lgm_oracle_render_batch(B, V, N, fp(g), fp(views), fp(projs), float(tanfov), float(tanfov),
                                        float(scale_modifier), fp(bgv), H, W, fp(color), fp(depth), fp(alpha),
                                        stats.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), fp(d_image),
                                        fp(d_depth), fp(d_alpha), fp(dg), int(nthreads))
+    lib(f64).lgm_oracle_set_tile_threads(1)
     if rc != 0:
         raise RuntimeError("oracle render failed")
     out = {"image": color, "depth": depth, "alpha": alpha, "K": int(stats[0]), "evals": int(stats[1])}
@@ -132,3 +141,17 @@ def tile_lists(g_scene, view16, proj16, tanfov: float, H: int, W: int, scale_mod
     ids = np.zeros(max(K, 1), np.int32)
     lib().lgm_oracle_tile_lists(*args, ids.ctypes.data_as(i32), K)
     return ts, ids[:K]
+
+
+def forward_state(g_scene, view16, proj16, tanfov: float, H: int, W: int, scale_modifier: float = 1.0):
+    """Per-pixel forward state of one view: (n_contrib [H,W] int32, final_T [H,W] float32, K)."""
+    g = _c(g_scene)
+    N = g.shape[0]
+    nc = np.zeros((H, W), np.int32)
+    ft = np.zeros((H, W), np.float32)
+    K = lib().lgm_oracle_forward_state(N, _f(g), _f(_c(view16).reshape(16)), _f(_c(proj16).reshape(16)),
+                                       float(tanfov), float(tanfov), float(scale_modifier), H, W,
+                                       nc.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _f(ft))
+    if K < 0:
+        raise RuntimeError("oracle forward_state failed")
+    return nc, ft, int(K)

@@ -45,6 +45,15 @@ typedef float real;
 #define BLOCK_X 16
 #define BLOCK_Y 16
 
+#include <omp.h>
+
+/* Threads over the Gaussians / tiles of ONE view (preprocess, per-tile sort, render_fwd / render_bwd), nested
+ * inside the batch's threads over views, for the CPU baseline on all host cores (bench.py cpu_baseline).
+ * 1 (default) keeps the sequential order. The backward then accumulates into per-thread double records, summed in
+ * thread order. */
+static int g_tile_threads = 1;
+void lgm_oracle_set_tile_threads(int n) { g_tile_threads = n > 1 ? n : 1; }
+
 /* ---------- small glm-style helpers (glm mat3 is column-major: m[col][row]) ---------- */
 typedef struct { real m[3][3]; } mat3;
 
@@ -163,6 +172,7 @@ static int cmp_u64(const void *a, const void *b) {
 }
 
 static void preprocess(view_state *S) {
+#pragma omp parallel for schedule(static, 256) num_threads(g_tile_threads)
     for (int i = 0; i < S->N; i++) {
         const real *gi = S->g + 14 * (size_t)i;
         S->radii[i] = 0;
@@ -230,6 +240,7 @@ static void bin_and_sort(view_state *S) {
                 S->keys[S->tile_start[t] + cnt[t]++] = ((uint64_t)db << 32) | (uint32_t)i;
             }
     }
+#pragma omp parallel for schedule(dynamic, 4) num_threads(g_tile_threads)
     for (int t = 0; t < T; t++)
         qsort(S->keys + S->tile_start[t], (size_t)(S->tile_start[t + 1] - S->tile_start[t]), sizeof(uint64_t), cmp_u64);
     free(cnt);
@@ -239,9 +250,10 @@ static void render_fwd(view_state *S, const real *bg, real *out_color, real *out
                        long long *evals) {
     const int H = S->H, W = S->W;
     long long ev = 0;
-    for (int ty = 0; ty < S->gy; ty++)
-        for (int tx = 0; tx < S->gx; tx++) {
-            const int t = ty * S->gx + tx;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(g_tile_threads) reduction(+ : ev)
+    for (int t = 0; t < S->gx * S->gy; t++) {
+        {
+            const int tx = t % S->gx, ty = t / S->gx;
             const int s0 = S->tile_start[t], s1 = S->tile_start[t + 1];
             for (int ly = 0; ly < BLOCK_Y; ly++)
                 for (int lx = 0; lx < BLOCK_X; lx++) {
@@ -276,6 +288,7 @@ static void render_fwd(view_state *S, const real *bg, real *out_color, real *out
                     out_alpha[pid] = 1 - T;
                 }
         }
+    }
     if (evals) *evals += ev;
 }
 
@@ -283,12 +296,20 @@ static void render_fwd(view_state *S, const real *bg, real *out_color, real *out
 typedef struct { double m2[2], con[3], op, col[3], dep; } g2d;
 
 static void render_bwd(view_state *S, const real *bg, const real *dLdc, const real *dLdd, const real *dLda,
-                       g2d *acc) {
+                       g2d *acc_out) {
     const int H = S->H, W = S->W;
     const real ddelx_dx = (real)(0.5 * W), ddely_dy = (real)(0.5 * H);
-    for (int ty = 0; ty < S->gy; ty++)
-        for (int tx = 0; tx < S->gx; tx++) {
-            const int t = ty * S->gx + tx;
+    const int nthr = g_tile_threads;
+    g2d *accs = acc_out;
+    if (nthr > 1) {
+        accs = (g2d *)calloc((size_t)nthr * (S->N > 0 ? S->N : 1), sizeof(g2d));
+        if (!accs) { accs = acc_out; }
+    }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(accs == acc_out ? 1 : nthr)
+    for (int t = 0; t < S->gx * S->gy; t++) {
+        g2d *acc = accs == acc_out ? acc_out : accs + (size_t)omp_get_thread_num() * S->N;
+        {
+            const int tx = t % S->gx, ty = t / S->gx;
             const int s0 = S->tile_start[t];
             for (int ly = 0; ly < BLOCK_Y; ly++)
                 for (int lx = 0; lx < BLOCK_X; lx++) {
@@ -350,6 +371,21 @@ static void render_bwd(view_state *S, const real *bg, const real *dLdc, const re
                     }
                 }
         }
+    }
+    if (accs != acc_out) {
+        for (int k = 0; k < nthr; k++) {
+            const g2d *a = accs + (size_t)k * S->N;
+            for (int i = 0; i < S->N; i++) {
+                g2d *o = acc_out + i;
+                o->m2[0] += a[i].m2[0]; o->m2[1] += a[i].m2[1];
+                o->con[0] += a[i].con[0]; o->con[1] += a[i].con[1]; o->con[2] += a[i].con[2];
+                o->op += a[i].op;
+                o->col[0] += a[i].col[0]; o->col[1] += a[i].col[1]; o->col[2] += a[i].col[2];
+                o->dep += a[i].dep;
+            }
+        }
+        free(accs);
+    }
 }
 
 /* cov2D backward + projection backward + cov3D backward */
@@ -532,6 +568,7 @@ int lgm_oracle_render_batch(int B, int V, int N, const real *g, const real *view
     }
     int err = 0;
     long long st[2] = {0, 0};
+    if (g_tile_threads > 1) omp_set_max_active_levels(2);
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : err)
     for (int bv = 0; bv < BV; bv++) {
         const int b = bv / V;
@@ -617,5 +654,47 @@ long long lgm_oracle_tile_lists(int N, const real *g, const real *view, const re
     if (ids && K <= ids_cap)
         for (long long k = 0; k < K; k++) ids[k] = (int)(uint32_t)S.keys[k];
     free(S.radii); free(S.xy); free(S.depth); free(S.conic); free(S.cov3); free(S.rect); free(S.keys);
+    return K;
+}
+
+/*
+ * Forward state of one view (what upstream's imgBuffer keeps for the backward): per-pixel n_contrib (1 + list
+ * position of the last accepted entry) and final transmittance, [H,W] each. Returns K or -1.
+ */
+long long lgm_oracle_forward_state(int N, const real *g, const real *view, const real *proj, real tanfovx,
+                                   real tanfovy, real scale_modifier, int H, int W, int *n_contrib, real *final_T) {
+    const size_t P = (size_t)H * W;
+    real *c = (real *)calloc(3 * P, sizeof(real)), *d = (real *)calloc(P, sizeof(real)),
+         *a = (real *)calloc(P, sizeof(real));
+    view_state S;
+    memset(&S, 0, sizeof(S));
+    S.N = N; S.H = H; S.W = W;
+    S.gx = (W + BLOCK_X - 1) / BLOCK_X;
+    S.gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+    S.tanx = tanfovx; S.tany = tanfovy;
+    S.fy = H / (2.0f * tanfovy);
+    S.fx = W / (2.0f * tanfovx);
+    S.mod = scale_modifier;
+    S.g = g; S.view = view; S.proj = proj;
+    const size_t n = N > 0 ? (size_t)N : 1;
+    S.radii = (int *)calloc(n, sizeof(int));
+    S.xy = (real *)calloc(2 * n, sizeof(real));
+    S.depth = (real *)calloc(n, sizeof(real));
+    S.conic = (real *)calloc(4 * n, sizeof(real));
+    S.cov3 = (real *)calloc(6 * n, sizeof(real));
+    S.rect = (int *)calloc(4 * n, sizeof(int));
+    S.tile_start = (int *)calloc((size_t)S.gx * S.gy + 1, sizeof(int));
+    S.final_T = final_T;
+    S.n_contrib = n_contrib;
+    long long K = -1;
+    if (c && d && a && S.radii && S.xy && S.depth && S.conic && S.cov3 && S.rect && S.tile_start) {
+        const real bg[3] = {0, 0, 0};
+        preprocess(&S);
+        bin_and_sort(&S);
+        render_fwd(&S, bg, c, d, a, NULL);
+        K = S.K;
+    }
+    free(S.radii); free(S.xy); free(S.depth); free(S.conic); free(S.cov3); free(S.rect);
+    free(S.tile_start); free(S.keys); free(c); free(d); free(a);
     return K;
 }

@@ -34,8 +34,15 @@ def main():
         ("mv_c128_h4_f4", "mv", dict(dim=128, num_heads=4, num_frames=4, skip_scale=0.5 ** 0.5), (4, 128, 16, 16)),
         ("mv_c256_h4_f4", "mv", dict(dim=256, num_heads=4, num_frames=4, skip_scale=0.5 ** 0.5), (4, 256, 8, 8)),
         ("mv_c128_h4_f6", "mv", dict(dim=128, num_heads=4, num_frames=6, skip_scale=0.5 ** 0.5), (6, 128, 10, 10)),
+        # LGM 'big' (6 input views at 320 -> 20^2 at the D=64 level): L = 6 * 20 * 20 = 2400 tokens at D = 32 and 64
+        ("mv_c64_h2_f6_l2400", "mv", dict(dim=64, num_heads=2, num_frames=6, skip_scale=0.5 ** 0.5), (6, 64, 20, 20)),
+        ("mv_c128_h2_f6_l2400", "mv", dict(dim=128, num_heads=2, num_frames=6, skip_scale=0.5 ** 0.5),
+         (6, 128, 20, 20)),
     ]
+    only = set(sys.argv[1:])  # optional: regenerate only the named cases
     for name, kind, kw, shape in cases:
+        if only and name not in only:
+            continue
         g = torch.Generator().manual_seed(zlib.crc32(name.encode()))
         if kind == "memeff":
             m = MemEffAttention(kw["dim"], kw["num_heads"], qkv_bias=False, proj_bias=True)

@@ -42,7 +42,7 @@ def _module(meta):
 
 
 def test_golden_present():
-    assert len(GOLDEN) >= 6
+    assert len(GOLDEN) >= 8
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=lambda p: os.path.basename(p)[5:-4])
@@ -120,6 +120,12 @@ def test_module_bf16_autocast(cuda, path):
 SHAPES = [  # B, L, H, D -- LGM levels (4 views x 8^2 / 16^2 / 32^2 tokens, D = 64 / 64 / 32) and ragged edges
     (1, 256, 16, 64), (2, 1024, 16, 64), (1, 4096, 16, 32), (1, 1, 2, 32), (3, 65, 2, 64), (2, 100, 3, 128),
     (1, 17, 1, 32), (2, 600, 4, 32), (2, 4100, 16, 32),  # the last one: two query sub-tiles per wave + a tail
+    # LGM 'big' (BASELINE config 4: 6 input views at 320, core/unet.py:35-49): L = 6 x 40^2 at C = 512 (D = 32),
+    # 6 x 20^2 and 6 x 10^2 at C = 1024 (D = 64)
+    (1, 9600, 16, 32), (1, 2400, 16, 64), (1, 600, 16, 64),
+    # D = 64 with two query sub-tiles per wave (ceil(L/128) * B * H >= 512): LGM's default training level
+    # (B = 8 is sharded; 4 x 1024 crosses the threshold) and the 'big' 2400-token level at B = 2
+    (4, 1024, 16, 64), (2, 2400, 16, 64),
 ]
 
 

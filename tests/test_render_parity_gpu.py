@@ -1,0 +1,218 @@
+"""GPU parity of the PRODUCTION render configuration and bit-exact integer parity of the binning.
+
+Production configuration = what LGM (core/models.py:141-153) and bench.py call: GaussianRenderer.render (the
+image clamped in-kernel as core/gs.py:87) and a backward of image and alpha only (d_depth is None, so
+k_render_bwd<false> runs, the kernel the benchmark times). The oracle is given torch's clamp gradient explicitly:
+d_image is masked where the fp64 forward's unclamped image lies outside [0, 1] (inclusive bounds, torch's
+clamp backward); pixels within 1e-5 of a bound are given zero upstream gradient on both sides, so an fp32
+rounding of the image across the bound cannot flip the mask between the two implementations.
+
+Integer parity (bit-exact, no tolerance): per view the GPU's radii equal the oracle's, the reference pair count
+K (upstream's num_rendered) equals the oracle's, and with exact culling disabled (LGM_RENDER_NO_CULL) every
+tile's sorted id list and every pixel's n_contrib equal the oracle's. With culling on, every GPU tile list is the
+oracle's list with the provably-skipped pairs removed, in the same order.
+
+Tolerances for floats are those of tests/test_render_gpu.py (forward 1e-4 rel L2; gradients within
+max(1e-4, 2 x the fp32 oracle's own error) of fp64).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from lgm_amd import GaussianRenderer, Options, _native
+from lgm_amd.gs import forward_state
+from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads
+from lgm_amd.cameras import orbit_cameras
+from tests.render_cases import TAN, rel_l2, scene, upstream
+
+pytestmark = pytest.mark.gpu
+
+FWD_TOL = 1e-4
+BWD_TOL = 1e-4
+BOUND_EPS = 1e-5  # pixels this close to a clamp bound get zero upstream gradient on both sides
+GROUPS = {"mean": slice(0, 3), "opacity": slice(3, 4), "scale": slice(4, 7), "rot": slice(7, 11), "rgb": slice(11, 14)}
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "render_*.npz")))
+
+
+def _clamp_masked_grads(O, g, cv, cvp, H, W, bg, d_img, mod=1.0):
+    """The upstream image gradient after torch's clamp(0, 1) backward, from the fp64 forward's unclamped image;
+    near-bound pixels zeroed."""
+    ref = O.render(g.numpy(), cv.numpy(), cvp.numpy(), TAN, H, W, bg.numpy(), scale_modifier=mod, f64=True)
+    img = ref["image"]
+    inside = (img >= 0.0) & (img <= 1.0)
+    near = (np.abs(img) < BOUND_EPS) | (np.abs(img - 1.0) < BOUND_EPS)
+    return torch.from_numpy((d_img.numpy() * (inside & ~near)).astype(np.float32)), \
+        torch.from_numpy((~near).astype(np.float32))
+
+
+def _production(cuda, g, cv, cvp, H, W, bg, d_img, d_alpha, keep, mod=1.0):
+    """GaussianRenderer.render + backward of image and alpha (LGM's loss inputs) on the GPU."""
+    opt = Options(output_size=H)
+    r = GaussianRenderer(opt)
+    gd = g.to(cuda).requires_grad_(True)
+    cp = torch.zeros(cv.shape[0], cv.shape[1], 3, device=cuda)
+    out = r.render(gd, cv.to(cuda), cvp.to(cuda), cp, bg_color=bg.to(cuda), scale_modifier=mod)
+    assert set(out) >= {"image", "alpha"}
+    # keep: near-bound pixels excluded from the loss (their clamp mask is rounding-ambiguous)
+    torch.autograd.backward([out["image"], out["alpha"]], [d_img.to(cuda) * keep.to(cuda), d_alpha.to(cuda)])
+    torch.cuda.synchronize()
+    return {"image": out["image"].detach().cpu().numpy(), "alpha": out["alpha"].detach().cpu().numpy(),
+            "d_gaussians": gd.grad.cpu().numpy()}
+
+
+def _check(O, out, g, cv, cvp, H, W, bg, d_img_masked, d_alpha, mod=1.0):
+    ref = O.render(g.numpy(), cv.numpy(), cvp.numpy(), TAN, H, W, bg.numpy(), scale_modifier=mod,
+                   d_image=d_img_masked.numpy(), d_alpha=d_alpha.numpy())
+    truth = O.render(g.numpy(), cv.numpy(), cvp.numpy(), TAN, H, W, bg.numpy(), scale_modifier=mod,
+                     d_image=d_img_masked.numpy(), d_alpha=d_alpha.numpy(), f64=True)["d_gaussians"]
+    e = rel_l2(out["image"], np.clip(ref["image"], 0.0, 1.0))
+    assert e < FWD_TOL, f"image: rel L2 {e:.3e}"
+    e = rel_l2(out["alpha"], ref["alpha"])
+    assert e < FWD_TOL, f"alpha: rel L2 {e:.3e}"
+    for name, sl in GROUPS.items():
+        e_gpu = rel_l2(out["d_gaussians"][..., sl], truth[..., sl])
+        e_o32 = rel_l2(ref["d_gaussians"][..., sl], truth[..., sl])
+        assert e_gpu < max(BWD_TOL, 2.0 * e_o32), f"d_{name}: GPU vs fp64 {e_gpu:.3e}, fp32 oracle {e_o32:.3e}"
+
+
+PROD_CASES = [
+    # B, N, V, H, mod, elevation, stretch colours outside [0, 1] (exercises the clamp)
+    (1, 300, 2, 64, 1.0, 0.0, False),
+    (2, 2000, 3, 64, 1.0, 15.0, False),
+    (1, 3000, 2, 48, 0.7, -20.0, True),
+    (2, 1500, 2, 128, 1.3, 20.0, True),
+    (1, 8000, 4, 128, 1.0, -15.0, True),
+]
+
+
+@pytest.mark.parametrize("B,N,V,H,mod,elev,stretch", PROD_CASES)
+def test_production_render_parity(cuda, oracle_mod, B, N, V, H, mod, elev, stretch):
+    g, cv, cvp = scene(B=B, N=N, V=V, seed=N + V + 3, elevation=elev)
+    if stretch:
+        g[..., 11:14] = g[..., 11:14] * 2.2 - 0.6
+    d_img, _, d_alpha, bg = upstream(B, V, H, H, seed=N)
+    d_m, keep = _clamp_masked_grads(oracle_mod, g, cv, cvp, H, H, bg, d_img, mod)
+    out = _production(cuda, g, cv, cvp, H, H, bg, d_img, d_alpha, keep, mod)
+    _check(oracle_mod, out, g, cv, cvp, H, H, bg, d_m, d_alpha, mod)
+
+
+def test_production_cfg3_bench_inputs(cuda, oracle_mod):
+    """BASELINE config 3 with bench.py's exact inputs: scene seed 1 (rank 0), upstream gradients seed 1001."""
+    g = synthetic_gaussians(1, 100_000, seed=1)
+    cv, cvp, _ = orbit_cameras(6)
+    cv, cvp = cv[None], cvp[None]
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(1, 6, 256, 256, seed=1001)
+    d_m, keep = _clamp_masked_grads(oracle_mod, g, cv, cvp, 256, 256, bg, d_img)
+    out = _production(cuda, g, cv, cvp, 256, 256, bg, d_img, d_alpha, keep)
+    _check(oracle_mod, out, g, cv, cvp, 256, 256, bg, d_m, d_alpha)
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=lambda p: os.path.basename(p)[7:-4])
+def test_golden_fixture(cuda, oracle_mod, path):
+    """Each committed fixture (tests/golden/render_*.npz, elevated cameras included): forward vs its stored
+    outputs, gradients (with its stored d_depth) vs its stored fp32 oracle gradient within max(1e-4, 2 x that
+    gradient's own error against a live fp64 evaluation)."""
+    from lgm_amd.gs import rasterize
+    z = np.load(path)
+    g = torch.from_numpy(z["gaussians"])
+    H, W = int(z["H"]), int(z["W"])
+    tan, mod = float(z["tanfov"]), float(z["scale_modifier"])
+    gd = g.to(cuda).requires_grad_(True)
+    img, dep, alp = rasterize(gd, torch.from_numpy(z["cam_view"]).to(cuda), torch.from_numpy(z["cam_view_proj"]).to(cuda),
+                              torch.from_numpy(z["bg"]).to(cuda), tan, tan, H, W, mod)
+    loss = (img * torch.from_numpy(z["d_image"]).to(cuda)).sum() + (dep * torch.from_numpy(z["d_depth"]).to(cuda)).sum() \
+        + (alp * torch.from_numpy(z["d_alpha"]).to(cuda)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    for k, t in (("image", img), ("depth", dep), ("alpha", alp)):
+        e = rel_l2(t.detach().cpu().numpy(), z[k])
+        assert e < FWD_TOL, f"{k}: rel L2 {e:.3e}"
+    truth = oracle_mod.render(z["gaussians"], z["cam_view"], z["cam_view_proj"], tan, H, W, z["bg"], mod,
+                              d_image=z["d_image"], d_depth=z["d_depth"], d_alpha=z["d_alpha"], f64=True)["d_gaussians"]
+    dg = gd.grad.cpu().numpy()
+    for name, sl in GROUPS.items():
+        e_gpu = rel_l2(dg[..., sl], truth[..., sl])
+        e_fix = rel_l2(z["d_gaussians"][..., sl], truth[..., sl])
+        assert e_gpu < max(BWD_TOL, 2.0 * e_fix), f"d_{name}: {e_gpu:.3e} vs fixture {e_fix:.3e}"
+
+
+# ---------------------------------------------------------------------------------------------- integer parity
+INT_CASES = {
+    "cfg2": dict(N=50_000, V=1, H=256, seed=0, elevation=0.0),
+    "cfg3": dict(N=100_000, V=6, H=256, seed=1, elevation=0.0),
+    "elevated": dict(N=20_000, V=3, H=128, seed=5, elevation=20.0),
+    "ragged": dict(N=7_000, V=2, H=72, seed=6, elevation=-15.0),
+}
+
+
+def _ties_scene():
+    g, cv, cvp = scene(N=3000, V=1, seed=3000)
+    g[..., 2] = 0.0  # a flat layer facing the azimuth-0 camera: every depth equal, order decided by id
+    g[..., 0:2] *= 0.6
+    return g, cv, cvp
+
+
+def _case(name):
+    if name == "ties":
+        g, cv, cvp = _ties_scene()
+        return g, cv, cvp, 48
+    c = INT_CASES[name]
+    g, cv, cvp = scene(N=c["N"], V=c["V"], seed=c["seed"], elevation=c["elevation"])
+    return g, cv, cvp, c["H"]
+
+
+@pytest.mark.parametrize("name", list(INT_CASES) + ["ties"])
+def test_integer_parity_radii_and_K(cuda, oracle_mod, name):
+    g, cv, cvp, H = _case(name)
+    st = forward_state(g.to(cuda), cv.to(cuda), cvp.to(cuda), TAN, TAN, H, H)
+    V = cv.shape[1]
+    K_sum = 0
+    for v in range(V):
+        pre = oracle_mod.preprocess(g[0].numpy(), cv[0, v].numpy(), cvp[0, v].numpy(), TAN, H, H)
+        bad = np.nonzero(st["radii"][0, v] != pre["radii"])[0]
+        assert bad.size == 0, f"view {v}: {bad.size} radii differ, e.g. ids {bad[:8]}"
+        K_sum += pre["K"]
+    assert st["K_reference"] == K_sum, (st["K_reference"], K_sum)
+    assert st["K_binned"] == int(st["tile_counts"].sum())
+
+
+@pytest.mark.parametrize("name", list(INT_CASES) + ["ties"])
+def test_integer_parity_tile_lists(cuda, oracle_mod, name):
+    """NO_CULL: the GPU's tile lists and n_contrib ARE the oracle's (upstream's 3-sigma rects). Culled (the
+    product default): each GPU list is an in-order subsequence of the oracle's."""
+    g, cv, cvp, H = _case(name)
+    V = cv.shape[1]
+    L = _native.lib()
+    try:
+        L.lgm_render_set_flags(1)  # LGM_RENDER_NO_CULL
+        full = forward_state(g.to(cuda), cv.to(cuda), cvp.to(cuda), TAN, TAN, H, H, lists=True)
+    finally:
+        L.lgm_render_set_flags(0)
+    culled = forward_state(g.to(cuda), cv.to(cuda), cvp.to(cuda), TAN, TAN, H, H, lists=True)
+    T = full["tile_counts"].shape[-1]
+    nc_mismatch = 0
+    for v in range(V):
+        ts, ids = oracle_mod.tile_lists(g[0].numpy(), cv[0, v].numpy(), cvp[0, v].numpy(), TAN, H, H)
+        counts = np.diff(ts)
+        assert np.array_equal(full["tile_counts"][0, v], counts), f"view {v}: tile counts differ"
+        assert np.array_equal(full["ids"][0][v], ids), f"view {v}: sorted tile lists differ"
+        # culled lists: in-order subsequences of the full ones
+        cc = culled["tile_counts"][0, v]
+        assert np.all(cc <= counts)
+        off_c = np.concatenate([[0], np.cumsum(cc)])
+        for t in range(T):
+            sub = culled["ids"][0][v][off_c[t]:off_c[t + 1]]
+            lst = ids[ts[t]:ts[t + 1]]
+            idx = {int(x): k for k, x in enumerate(lst)}
+            ks = np.array([idx.get(int(x), -1) for x in sub])
+            assert np.all(ks >= 0) and np.all(np.diff(ks) > 0), f"view {v} tile {t}: not an in-order subsequence"
+        nc, _, _ = oracle_mod.forward_state(g[0].numpy(), cv[0, v].numpy(), cvp[0, v].numpy(), TAN, H, H)
+        nc_mismatch += int((full["n_contrib"][0, v] != nc).sum())
+    # n_contrib depends on the 1/255 and T < 1e-4 decisions, i.e. on exp(): the GPU evaluates v_exp_f32(power *
+    # log2 e), the oracle libm expf. A decision flips only where alpha lands within ~1e-7 of a threshold.
+    npix = V * H * H
+    print(f"{name}: n_contrib differs at {nc_mismatch} of {npix} pixels")
+    assert nc_mismatch <= max(2, npix // 100_000), f"{nc_mismatch} of {npix} pixels differ in n_contrib"

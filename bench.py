@@ -12,6 +12,7 @@ Secondary objects on the same line:
     all-reduce of dL/dgaussians [1,N,14] (SURVEY §8(e)); at G = 1 this is exactly BASELINE config 3;
   * "cfg2": 50k Gaussians x 1 view x 256^2 forward only (BASELINE config 2), rank 0;
   * "attention": LGM's heaviest MVAttention level, bf16 fwd+bwd, MFMA and exp rooflines;
+  * "cfg4": the attention blocks and the 20-view 512^2 render of one LGM 'big' forward (BASELINE config 4);
   * "roofline": the dominant kernel priced with SURVEY §8(d)'s algorithmic bytes over its HIP-event time;
   * "cpu_baseline": the CPU oracle port on all host cores (rank 0, N = 1).
 
@@ -23,7 +24,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import subprocess
 import sys
 import time
@@ -201,6 +201,68 @@ def cfg2_bench(dev, steps):
             "Mpixels_per_s": round(steps * RES * RES / el / 1e6, 2)}
 
 
+# LGM 'big' at BASELINE config 4 (core/options.py:93-103 with 6 input views at input_size 320, splat 160): the
+# MVAttention calls of one UNet forward (core/unet.py:240-290; down levels 3-5 x 2 layers, mid x 1, up levels 0-2 x
+# 3 layers) as (channels, spatial side) and the render of 20 views at 512^2 of N = 6 * 160^2 Gaussians.
+CFG4_ATTN = [(512, 40)] * 2 + [(1024, 20)] * 2 + [(1024, 10)] * 2 + [(1024, 10)] + [(1024, 10)] * 3 + \
+    [(1024, 20)] * 3 + [(512, 40)] * 3
+CFG4_VIEWS, CFG4_FRAMES, CFG4_N, CFG4_RES = 20, 6, 6 * 160 * 160, 512
+
+
+def cfg4_bench(dev, steps):
+    """The hot-path share of BASELINE config 4 (LGM 'big' forward, inference): the 16 MVAttention blocks at their
+    cfg4 shapes (GroupNorm + qkv + HIP flash attention + proj + residual, bf16 autocast, random init: there are no
+    weights offline) and the GaussianRenderer forward of 20 views at 512^2. The UNet's convolutions / ResNet blocks
+    are plain torch and out of scope; their time is not included."""
+    import torch
+
+    from lgm_amd import GaussianRenderer, Options
+    from lgm_amd.attention import MVAttention
+    from lgm_amd.cameras import orbit_cameras
+    from lgm_amd.synthetic import synthetic_gaussians
+    torch.manual_seed(4)
+    mods = {}
+    xs = []
+    for C, S in CFG4_ATTN:
+        if C not in mods:
+            mods[C] = MVAttention(C, 16, num_frames=CFG4_FRAMES, skip_scale=0.5 ** 0.5).to(dev).eval()
+        xs.append((mods[C], torch.randn(CFG4_FRAMES, C, S, S, device=dev)))
+
+    def attn_pass():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            for m, x in xs:
+                m(x)
+
+    r = GaussianRenderer(Options(output_size=CFG4_RES))
+    g = synthetic_gaussians(1, CFG4_N, seed=4).to(dev)
+    cv, cvp, cp = (t[None].to(dev) for t in orbit_cameras(CFG4_VIEWS))
+    bg = torch.ones(3, device=dev)
+
+    def render_pass():
+        with torch.no_grad():
+            r.render(g, cv, cvp, cp, bg_color=bg)
+
+    def timed(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        return 1e3 * (time.perf_counter() - t0) / steps
+
+    ms_attn, ms_render = timed(attn_pass), timed(render_pass)
+    flops = sum(4.0 * (CFG4_FRAMES * S * S) ** 2 * C for C, S in CFG4_ATTN)  # QK^T + PV per call (B = 1)
+    px = CFG4_VIEWS * CFG4_RES * CFG4_RES
+    return {"workload": "cfg4 hot path: LGM 'big' (6 input views at 320 -> N = 153,600 Gaussians) -- 16 MVAttention "
+                        "blocks (L = 9600 @ C512 x5, 2400 @ C1024 x5, 600 @ C1024 x6; bf16, forward) + render of 20 "
+                        "views at 512^2 (forward); UNet convolutions excluded",
+            "attention_ms": round(ms_attn, 4), "attention_core_tflops": round(flops / ms_attn / 1e9, 1),
+            "render_ms": round(ms_render, 4), "render_Mpixels_per_s": round(px / ms_render / 1e3, 1),
+            "ms_total": round(ms_attn + ms_render, 4)}
+
+
 def run(args):
     import torch
 
@@ -331,6 +393,8 @@ def run(args):
 
     if rank == 0:
         result["cfg2"] = cfg2_bench(dev, args.steps)
+        if not args.no_cfg4:
+            result["cfg4"] = cfg4_bench(dev, max(3, args.steps // 10))
         if not args.no_attention:
             result["attention"] = attention_bench(dev)
         if world == 1 and not args.no_cpu_baseline:
@@ -340,18 +404,8 @@ def run(args):
     D.finalize(info)
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _spawned(local_rank, world, port, argv):
-    """Child rank of a self-launched multi-GPU run: torchrun's environment, then the ordinary entry point."""
-    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
-                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _rank_main(argv):
+    """A rank of a self-launched multi-GPU run (lgm_amd.dist.spawn_ranks set torchrun's environment)."""
     run(parse(argv))
 
 
@@ -363,6 +417,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-attention", action="store_true", help="skip the secondary attention measurement")
+    ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 (LGM 'big') hot-path measurement")
     return ap.parse_args(argv)
 
 
@@ -375,9 +430,8 @@ def main():
         run(args)
     elif args.gpus > 1:
         # no launcher: start the ranks here, before anything touches the GPU (children, not an exec)
-        import torch.multiprocessing as mp
-        mp.start_processes(_spawned, args=(args.gpus, _free_port(), sys.argv[1:]), nprocs=args.gpus,
-                           start_method="spawn")
+        from lgm_amd import dist as D
+        D.spawn_ranks(_rank_main, args.gpus, sys.argv[1:])
     else:
         run(args)
 

@@ -86,6 +86,30 @@ def timed_steps(step: Callable[[], None], steps: int, info: RankInfo, sync: Call
     return max_over_ranks(time.perf_counter() - t0, info, device)
 
 
+def _spawned_rank(local_rank, world, port, target, args):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    target(*args)
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(target: Callable, world: int, *args) -> None:
+    """One process per rank on this node without an external launcher: each child gets torch.distributed.run's
+    environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and calls target(*args).
+    Started with the 'spawn' method, as fresh children: the caller must not have initialised the GPU (no exec of a
+    GPU-initialised process). Raises if any rank fails."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_spawned_rank, args=(world, free_port(), target, args), nprocs=world, start_method="spawn")
+
+
 def allreduce_scene_grads(grad, info: RankInfo):
     """View-sharded variant: when the V views of ONE scene are split over ranks
     (views shard_range(V, rank, world)), each rank's dL/dgaussians holds only its views' contributions; one

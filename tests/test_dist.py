@@ -81,6 +81,29 @@ def _run(mode, tmp):
     return [np.load(os.path.join(tmp, f"r{r}.npz")) for r in range(WORLD)]
 
 
+def _spawn_target(tmp):
+    info = D.rank_info()
+    D.init("gloo", info)
+    try:
+        t = torch.tensor([float(info.rank + 1)])
+        import torch.distributed as dist
+        dist.all_reduce(t)
+        np.savez(os.path.join(tmp, f"s{info.rank}.npz"), rank=info.rank, world=info.world, local=info.local,
+                 total=t.numpy(), addr=os.environ["MASTER_ADDR"])
+    finally:
+        D.finalize(info)
+
+
+def test_spawn_ranks_sets_launcher_env(tmp_path):
+    """bench.py --gpus N without torchrun: dist.spawn_ranks starts N ranks with torchrun's environment."""
+    D.spawn_ranks(_spawn_target, WORLD, str(tmp_path))
+    res = [np.load(os.path.join(tmp_path, f"s{r}.npz")) for r in range(WORLD)]
+    assert [int(r["rank"]) for r in res] == list(range(WORLD))
+    assert all(int(r["world"]) == WORLD and int(r["local"]) == int(r["rank"]) for r in res)
+    assert all(float(r["total"][0]) == WORLD * (WORLD + 1) / 2 for r in res)
+    assert all(str(r["addr"]) == "127.0.0.1" for r in res)
+
+
 def test_shard_range():
     for n in range(0, 20):
         for w in range(1, 9):

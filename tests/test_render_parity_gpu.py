@@ -110,6 +110,19 @@ def test_production_cfg3_bench_inputs(cuda, oracle_mod):
     _check(oracle_mod, out, g, cv, cvp, 256, 256, bg, d_m, d_alpha)
 
 
+def test_production_cfg4_512(cuda, oracle_mod):
+    """BASELINE config 4's render: N = 6 x 160^2 = 153,600 Gaussians at 512^2 (1,024 tiles per view). The batched
+    call renders 4 of the 20 orbit views (the oracle's fp64 check bounds the test's run time); production path."""
+    g = synthetic_gaussians(1, 153_600, seed=4)
+    cv, cvp, _ = orbit_cameras(20)
+    sel = [0, 3, 11, 17]
+    cv, cvp = cv[None, sel], cvp[None, sel]
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(1, len(sel), 512, 512, seed=44)
+    d_m, keep = _clamp_masked_grads(oracle_mod, g, cv, cvp, 512, 512, bg, d_img)
+    out = _production(cuda, g, cv, cvp, 512, 512, bg, d_img, d_alpha, keep)
+    _check(oracle_mod, out, g, cv, cvp, 512, 512, bg, d_m, d_alpha)
+
+
 @pytest.mark.parametrize("path", GOLDEN, ids=lambda p: os.path.basename(p)[7:-4])
 def test_golden_fixture(cuda, oracle_mod, path):
     """Each committed fixture (tests/golden/render_*.npz, elevated cameras included): forward vs its stored
@@ -216,3 +229,24 @@ def test_integer_parity_tile_lists(cuda, oracle_mod, name):
     npix = V * H * H
     print(f"{name}: n_contrib differs at {nc_mismatch} of {npix} pixels")
     assert nc_mismatch <= max(2, npix // 100_000), f"{nc_mismatch} of {npix} pixels differ in n_contrib"
+
+
+def test_exact_count_path_matches_slot_path_512(cuda, monkeypatch):
+    """The packed workspace (exact pair count first, one host sync; taken when the slot workspace exceeds the
+    budget) gives the slot path's forward bit for bit and its gradient up to float-atomic ordering, at cfg4's
+    512^2 (1,024 tiles per view) with 6 of the 20 views."""
+    from lgm_amd import gs as lgs
+    g = synthetic_gaussians(1, 153_600, seed=4)
+    cv, cvp, _ = orbit_cameras(20)
+    cv, cvp = cv[None, 0:20:4].contiguous(), cvp[None, 0:20:4].contiguous()
+    V = cv.shape[1]
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(1, V, 512, 512, seed=45)
+    keep = torch.ones(1)
+    outs = []
+    for budget in (None, 0):
+        monkeypatch.setattr(lgs, "_WS_BUDGET", budget)
+        outs.append(_production(cuda, g, cv, cvp, 512, 512, bg, d_img, d_alpha, keep))
+    slot, packed = outs
+    for k in ("image", "alpha"):
+        assert np.array_equal(slot[k], packed[k]), k
+    assert rel_l2(packed["d_gaussians"], slot["d_gaussians"]) < 1e-5

@@ -34,6 +34,11 @@ SIGNATURES = {
     "lgm_render_tile_lists": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp,
                                        _vp]),
     "lgm_render_pixel_state": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp]),
+    "lgm_gaussian_head_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp,
+                                           _c_size, _vp]),
+    "lgm_gaussian_head_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "lgm_gaussian_head_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                            _vp, _vp, _c_size, _vp]),
     "lgm_render_debug_counters": (_c_int, [_vp]),
     "lgm_render_set_flags": (_c_int, [_c_int]),
     "lgm_profiler_create": (_vp, []),

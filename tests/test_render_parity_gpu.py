@@ -249,4 +249,7 @@ def test_exact_count_path_matches_slot_path_512(cuda, monkeypatch):
     slot, packed = outs
     for k in ("image", "alpha"):
         assert np.array_equal(slot[k], packed[k]), k
-    assert rel_l2(packed["d_gaussians"], slot["d_gaussians"]) < 1e-5
+    # same sums in a different float-atomic order: within the gradient bar of the oracle tests
+    for name, sl in GROUPS.items():
+        e = rel_l2(packed["d_gaussians"][..., sl], slot["d_gaussians"][..., sl])
+        assert e < BWD_TOL, f"d_{name}: {e:.3e}"

@@ -60,13 +60,34 @@ int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians
                        int options, void *stream);
 
 /* Backward of all B x V renders (replaces B*V calls of _C.rasterize_gaussians_backward plus the autograd sum
- * over views). d_depth / d_alpha may be NULL (treated as zero). Writes d_gaussians [B,N,14] (overwrites).
+ * over views). d_image / d_depth / d_alpha may be NULL (treated as zero). Writes d_gaussians [B,N,14] (overwrites).
  * d_means2D [B,V,N,2] (screen-space gradients, what upstream returns for means2D) may be NULL. */
 int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
                         const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
                         float *d_gaussians, float *d_means2D, void *workspace, size_t workspace_bytes,
                         long long pair_capacity, int options, void *stream);
+
+/* Loss-fused variants for training (core/models.py:133-167): with gt_images [B,V,3,H,W] and gt_masks [B,V,1,H,W]
+ * (DEVICE fp32), the forward also composites the ground truth over bg (gt * mask + bg * (1 - mask)) and writes
+ * loss_out (DEVICE float[4]) = (loss_mse, mse_image, mse_alpha, psnr) with loss_mse = F.mse_loss(image, gt) +
+ * F.mse_loss(alpha, mask) and psnr = -10 log10(mse_image) -- per-tile partial sums inside the compositing kernel,
+ * one fixed-order reduction, no separate loss kernels. The backward seeds dL/dimage and dL/dalpha in-kernel from
+ * d_loss (DEVICE float[2] = dL/dmse_image, dL/dmse_alpha; both equal dL/dloss_mse for the plain sum) and the same
+ * ground truth: 2 (image - gt) d_loss[0] / numel(image) (image after the clamp when LGM_RENDER_CLAMP_IMAGE) and
+ * 2 (alpha - mask) d_loss[1] / numel(alpha), plus the optional d_image / d_alpha of other losses on the same
+ * outputs (e.g. LPIPS, core/models.py:150-158; NULL = none). Pass the same options to both. */
+int lgm_render_forward_loss(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                            const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
+                            float scale_modifier, float *image, float *depth, float *alpha, const float *gt_images,
+                            const float *gt_masks, float *loss_out, void *workspace, size_t workspace_bytes,
+                            long long pair_capacity, int options, void *stream);
+int lgm_render_backward_loss(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                             const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
+                             float scale_modifier, const float *d_image, const float *d_alpha,
+                             const float *gt_images, const float *gt_masks, const float *d_loss,
+                             float *d_gaussians, void *workspace, size_t workspace_bytes, long long pair_capacity,
+                             int options, void *stream);
 
 /* Inspection of the state a forward left in its workspace (the equivalent of upstream's saved binningBuffer /
  * imgBuffer: point_list + ranges, n_contrib, accum_alpha), for parity tests and debugging. Stream-ordered.
@@ -105,6 +126,8 @@ int lgm_render_debug_counters(unsigned long long *device_counters);
  * backward (autograd with retain_graph): its gradient accumulators are cleared first. The forward's binning
  * zeroes them, so a first backward needs no clearing pass. */
 #define LGM_RENDER_BACKWARD_AGAIN 4
+/* (internal) set by lgm_render_forward_loss / lgm_render_backward_loss; ignored in `options`. */
+#define LGM_RENDER_FUSED_LOSS 8
 
 /* Option flags (process-wide, default 0). LGM_RENDER_NO_CULL bins upstream's full 3-sigma tile rects instead of
  * dropping (Gaussian, tile) pairs where alpha < 1/255 is provable for every pixel; outputs are identical either

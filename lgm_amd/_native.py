@@ -31,6 +31,12 @@ SIGNATURES = {
     "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _c_ll, _vp, _c_size, _vp]),
     "lgm_attn_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "lgm_render_forward_loss": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float,
+                                         _c_float, _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _c_int,
+                                         _vp]),
+    "lgm_render_backward_loss": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float,
+                                          _c_float, _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll,
+                                          _c_int, _vp]),
     "lgm_render_tile_lists": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp,
                                        _vp]),
     "lgm_render_pixel_state": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp]),

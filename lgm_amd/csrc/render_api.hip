@@ -38,6 +38,9 @@ int check_common(int B, int V, int N, int H, int W, const void *g, const void *c
     d.counters = g_counters;
     d.flags = g_flags;
     d.options = 0;
+    d.gt_img = d.gt_mask = nullptr;
+    d.loss_part = d.loss_out = nullptr;
+    d.d_loss = nullptr;
     return LGM_OK;
 }
 
@@ -119,11 +122,14 @@ int lgm_render_count_pairs(int B, int V, int N, int H, int W, const float *gauss
                                true, (hipStream_t)stream);
 }
 
-int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
-                       const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
-                       float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
-                       void *workspace, size_t workspace_bytes, long long pair_capacity, long long *stats_out,
-                       int options, void *stream) {
+}  // extern "C"
+
+static int forward_impl(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                        const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
+                        float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
+                        const float *gt_images, const float *gt_masks, float *loss_out, void *workspace,
+                        size_t workspace_bytes, long long pair_capacity, long long *stats_out, int options,
+                        void *stream) {
     lgm::clear_error();
     lgm::Dims d;
     int rc = check_common(B, V, N, H, W, gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, scale_modifier, d);
@@ -141,12 +147,101 @@ int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians
         lgm::set_error("workspace too small (%zu < %zu)", workspace_bytes, L.total);
         return LGM_E_WORKSPACE;
     }
-    d.options = options;
     char *ws = (char *)workspace;
+    d.options = options & ~LGM_RENDER_FUSED_LOSS;
+    if (gt_images || gt_masks || loss_out) {
+        if (!gt_images || !gt_masks || !loss_out) {
+            lgm::set_error("fused loss needs gt_images, gt_masks and loss_out");
+            return LGM_E_INVALID;
+        }
+        d.options |= LGM_RENDER_FUSED_LOSS;
+        d.gt_img = gt_images;
+        d.gt_mask = gt_masks;
+        d.loss_part = (float *)(ws + L.lossp);
+        d.loss_out = loss_out;
+    }
     hipStream_t st = (hipStream_t)stream;
     rc = lgm::launch_binning(d, gaussians, cam_view, cam_view_proj, ws, L, radii_out, stats_out, false, st);
     if (rc) return rc;
-    return lgm::launch_render_fwd(d, gaussians, bg, image, depth, alpha, ws, L, st);
+    rc = lgm::launch_render_fwd(d, gaussians, bg, image, depth, alpha, ws, L, st);
+    if (rc || !(d.options & LGM_RENDER_FUSED_LOSS)) return rc;
+    return lgm::launch_loss_reduce(d, ws, L, st);
+}
+
+static int backward_impl(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                         const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
+                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
+                         const float *gt_images, const float *gt_masks, const float *d_loss, float *d_gaussians,
+                         float *d_means2D, void *workspace, size_t workspace_bytes, long long pair_capacity,
+                         int options, void *stream) {
+    lgm::clear_error();
+    lgm::Dims d;
+    int rc = check_common(B, V, N, H, W, gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, scale_modifier, d);
+    if (rc) return rc;
+    if (!bg || (N > 0 && !d_gaussians)) {
+        lgm::set_error("null pointer in backward");
+        return LGM_E_INVALID;
+    }
+    const lgm::Layout L = lgm::make_layout(B, V, N, H, W, pair_capacity);
+    if (!workspace || workspace_bytes < L.total) {
+        lgm::set_error("workspace too small (%zu < %zu)", workspace_bytes, L.total);
+        return LGM_E_WORKSPACE;
+    }
+    if (N == 0) return LGM_OK;
+    d.options = options & ~LGM_RENDER_FUSED_LOSS;
+    if (gt_images || gt_masks || d_loss) {
+        if (!gt_images || !gt_masks || !d_loss) {
+            lgm::set_error("fused loss backward needs gt_images, gt_masks and d_loss");
+            return LGM_E_INVALID;
+        }
+        d.options |= LGM_RENDER_FUSED_LOSS;
+        d.gt_img = gt_images;
+        d.gt_mask = gt_masks;
+        d.d_loss = d_loss;
+    }
+    return lgm::launch_render_bwd(d, gaussians, cam_view, cam_view_proj, bg, d_image, d_depth, d_alpha, d_gaussians,
+                                  d_means2D, (char *)workspace, L, (hipStream_t)stream);
+}
+
+extern "C" {
+
+int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                       const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
+                       float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
+                       void *workspace, size_t workspace_bytes, long long pair_capacity, long long *stats_out,
+                       int options, void *stream) {
+    return forward_impl(B, V, N, H, W, gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, scale_modifier,
+                        image, depth, alpha, radii_out, nullptr, nullptr, nullptr, workspace, workspace_bytes,
+                        pair_capacity, stats_out, options, stream);
+}
+
+int lgm_render_forward_loss(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                            const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
+                            float scale_modifier, float *image, float *depth, float *alpha, const float *gt_images,
+                            const float *gt_masks, float *loss_out, void *workspace, size_t workspace_bytes,
+                            long long pair_capacity, int options, void *stream) {
+    if (!gt_images || !gt_masks || !loss_out) {
+        lgm::set_error("null gt_images / gt_masks / loss_out");
+        return LGM_E_INVALID;
+    }
+    return forward_impl(B, V, N, H, W, gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, scale_modifier,
+                        image, depth, alpha, nullptr, gt_images, gt_masks, loss_out, workspace, workspace_bytes,
+                        pair_capacity, nullptr, options, stream);
+}
+
+int lgm_render_backward_loss(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
+                             const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
+                             float scale_modifier, const float *d_image, const float *d_alpha,
+                             const float *gt_images, const float *gt_masks, const float *d_loss,
+                             float *d_gaussians, void *workspace, size_t workspace_bytes, long long pair_capacity,
+                             int options, void *stream) {
+    if (!gt_images || !gt_masks || !d_loss) {
+        lgm::set_error("null gt_images / gt_masks / d_loss");
+        return LGM_E_INVALID;
+    }
+    return backward_impl(B, V, N, H, W, gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, scale_modifier,
+                         d_image, nullptr, d_alpha, gt_images, gt_masks, d_loss, d_gaussians, nullptr, workspace,
+                         workspace_bytes, pair_capacity, options, stream);
 }
 
 int lgm_render_tile_lists(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
@@ -197,23 +292,9 @@ int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussian
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
                         float *d_gaussians, float *d_means2D, void *workspace, size_t workspace_bytes,
                         long long pair_capacity, int options, void *stream) {
-    lgm::clear_error();
-    lgm::Dims d;
-    int rc = check_common(B, V, N, H, W, gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, scale_modifier, d);
-    if (rc) return rc;
-    if (!bg || !d_image || (N > 0 && !d_gaussians)) {
-        lgm::set_error("null pointer in backward");
-        return LGM_E_INVALID;
-    }
-    const lgm::Layout L = lgm::make_layout(B, V, N, H, W, pair_capacity);
-    if (!workspace || workspace_bytes < L.total) {
-        lgm::set_error("workspace too small (%zu < %zu)", workspace_bytes, L.total);
-        return LGM_E_WORKSPACE;
-    }
-    if (N == 0) return LGM_OK;
-    d.options = options;
-    return lgm::launch_render_bwd(d, gaussians, cam_view, cam_view_proj, bg, d_image, d_depth, d_alpha, d_gaussians,
-                                  d_means2D, (char *)workspace, L, (hipStream_t)stream);
+    return backward_impl(B, V, N, H, W, gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, scale_modifier,
+                         d_image, d_depth, d_alpha, nullptr, nullptr, nullptr, d_gaussians, d_means2D, workspace,
+                         workspace_bytes, pair_capacity, options, stream);
 }
 
 }  // extern "C"

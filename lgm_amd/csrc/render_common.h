@@ -26,7 +26,7 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 //   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
 struct Layout {
     size_t gP, gQ, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, cfin, ck, cklist, nck, cmask, accum,
-        misc, total;
+        lossp, misc, total;
     long long cap;
     int ck_region;  // backward checkpoint slots per region (8 regions; the forward shards tiles over them)
     bool slot;
@@ -58,6 +58,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.nck = take(BV * T * 4);
     L.cmask = take(BV * P);
     L.accum = take(BV * N * NACC * 4);
+    L.lossp = take(BV * T * 2 * 4);  // per-tile sums of squared image / alpha residuals (fused loss)
     L.total = o;
     return L;
 }
@@ -67,7 +68,13 @@ struct Dims {
     float tanx, tany, fx, fy, mod;
     unsigned long long *counters;  // optional device u64[8] work counters (see lgm_render_debug_counters), or null
     int flags;                     // LGM_RENDER_NO_CULL: bin upstream's full 3-sigma rects (no exact culling)
-    int options;                   // per-call LGM_RENDER_CLAMP_IMAGE
+    int options;                   // per-call LGM_RENDER_CLAMP_IMAGE / LGM_RENDER_FUSED_LOSS
+    // LGM_RENDER_FUSED_LOSS (core/models.py:138-160): ground truth [BV,3,P] / [BV,P], the per-tile loss partials
+    // (forward) and the gradients of the two MSE terms (backward)
+    const float *gt_img, *gt_mask;
+    float *loss_part;  // workspace: per-tile (image, alpha) sums of squared residuals
+    float *loss_out;   // DEVICE float[4]: loss_mse, mse_image, mse_alpha, psnr
+    const float *d_loss;  // DEVICE float[2]: dL/dmse_image, dL/dmse_alpha
 };
 
 // ------------------------------------------------------------------------------------------------------------
@@ -316,6 +323,9 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                    hipStream_t st);
 int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, float *image, float *depth,
                       float *alpha, char *ws, const Layout &L, hipStream_t st);
+// the fused loss's final reduction (after launch_render_fwd with LGM_RENDER_FUSED_LOSS): d.loss_out receives
+// (loss_mse, mse_image, mse_alpha, psnr)
+int launch_loss_reduce(const Dims &d, char *ws, const Layout &L, hipStream_t st);
 int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_view, const float *cam_view_proj,
                       const float *bg, const float *d_image, const float *d_depth, const float *d_alpha,
                       float *d_gaussians, float *d_means2D, char *ws, const Layout &L, hipStream_t st);

@@ -417,13 +417,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
             d.counters[8 + 8 * (size_t)tile + 7] = c_list;  // list entries staged (walked) by the forward
         }
     }
+    float lsq_img = 0.f, lsq_a = 0.f;  // fused loss: this pixel's squared residuals
     if (inside) {
         const size_t P = (size_t)d.H * d.W;
         const size_t pid = (size_t)d.W * py + px;
         final_T[bv * P + pid] = Tr;
         n_contrib[bv * P + pid] = last;
         float *img = out_img + (size_t)bv * 3 * P;
-        float c0 = C0 + Tr * bg[0], c1 = C1 + Tr * bg[1], c2 = C2 + Tr * bg[2];
+        // explicit FMAs: the fused loss's backward recomputes these values bit for bit from cfin and final_T
+        float c0 = fmaf(Tr, bg[0], C0), c1 = fmaf(Tr, bg[1], C1), c2 = fmaf(Tr, bg[2], C2);
         if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // core/gs.py:87, gradient mask kept for the backward
             auto in01 = [](float v) { return (v >= 0.f && v <= 1.f) ? 1u : 0u; };
             cmask[bv * P + pid] = (unsigned char)(in01(c0) | (in01(c1) << 1) | (in01(c2) << 2));
@@ -437,6 +439,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         out_depth[bv * P + pid] = D;
         out_alpha[bv * P + pid] = 1 - Tr;
         cfin[bv * P + pid] = make_float4(C0, C1, C2, D);  // pre-background totals for the backward
+        if (d.options & LGM_RENDER_FUSED_LOSS) {
+            // core/models.py:145-148: gt composited over the background, squared residuals of image and alpha
+            const float m = d.gt_mask[bv * P + pid];
+            const float *gi = d.gt_img + (size_t)bv * 3 * P;
+            const float r0 = c0 - (gi[pid] * m + bg[0] * (1.f - m));
+            const float r1 = c1 - (gi[P + pid] * m + bg[1] * (1.f - m));
+            const float r2 = c2 - (gi[2 * P + pid] * m + bg[2] * (1.f - m));
+            const float ra = (1 - Tr) - m;
+            lsq_img = r0 * r0 + r1 * r1 + r2 * r2;
+            lsq_a = ra * ra;
+        }
+    }
+    if (d.options & LGM_RENDER_FUSED_LOSS) {  // workgroup-uniform: per-tile partial sums, fixed order
+        __shared__ float sL[2][4];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            lsq_img += __shfl_xor(lsq_img, o, 64);
+            lsq_a += __shfl_xor(lsq_a, o, 64);
+        }
+        if (lane == 0) { sL[0][w] = lsq_img; sL[1][w] = lsq_a; }
+        __syncthreads();
+        if (tid < 2) d.loss_part[2 * (size_t)tile + tid] = ((sL[tid][0] + sL[tid][1]) + sL[tid][2]) + sL[tid][3];
+    }
+}
+
+// Fused loss, final reduction over the per-tile partials (one workgroup, fixed order):
+// out = (loss_mse, mse_image, mse_alpha, psnr) as core/models.py:148 (F.mse_loss twice) and :167 (psnr).
+__global__ __launch_bounds__(256) void k_loss_reduce(int M, const float *__restrict__ part, double n_img, double n_a,
+                                                     float *__restrict__ out) {
+    __shared__ double s[2][256];
+    const int t = threadIdx.x;
+    double a = 0.0, b = 0.0;
+    for (int k = t; k < M; k += 256) {
+        a += part[2 * (size_t)k];
+        b += part[2 * (size_t)k + 1];
+    }
+    s[0][t] = a;
+    s[1][t] = b;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h) {
+            s[0][t] += s[0][t + h];
+            s[1][t] += s[1][t + h];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const float mi = (float)(s[0][0] / n_img), ma = (float)(s[1][0] / n_a);
+        out[0] = mi + ma;
+        out[1] = mi;
+        out[2] = ma;
+        out[3] = -10.f * log10f(mi);
     }
 }
 
@@ -527,10 +581,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, dpd = 0.f, dpa = 0.f;
     float4 cf = make_float4(0.f, 0.f, 0.f, 0.f);
     if (inside) {
-        const float *di = d_img + (size_t)bv * 3 * P;
-        dp0 = di[pid];
-        dp1 = di[P + pid];
-        dp2 = di[2 * P + pid];
+        cf = cfin[bv * P + pid];
+        if (d_img) {
+            const float *di = d_img + (size_t)bv * 3 * P;
+            dp0 = di[pid];
+            dp1 = di[P + pid];
+            dp2 = di[2 * P + pid];
+        }
+        if (d.options & LGM_RENDER_FUSED_LOSS) {
+            // the MSE seeds (core/models.py:148): dL/dimage += 2 (image - gt) dL/dmse_image / numel, likewise alpha;
+            // image recomputed from the forward's totals exactly as the forward formed it
+            const float s_img = 2.f * d.d_loss[0] / (float)(3.0 * d.BV * (double)P);
+            const float s_a = 2.f * d.d_loss[1] / (float)((double)d.BV * P);
+            const float m = d.gt_mask[bv * P + pid];
+            const float *gi = d.gt_img + (size_t)bv * 3 * P;
+            float c0 = fmaf(T_final, bg[0], cf.x), c1 = fmaf(T_final, bg[1], cf.y), c2 = fmaf(T_final, bg[2], cf.z);
+            if (d.options & LGM_RENDER_CLAMP_IMAGE) {
+                c0 = fminf(fmaxf(c0, 0.f), 1.f);
+                c1 = fminf(fmaxf(c1, 0.f), 1.f);
+                c2 = fminf(fmaxf(c2, 0.f), 1.f);
+            }
+            dp0 += s_img * (c0 - (gi[pid] * m + bg[0] * (1.f - m)));
+            dp1 += s_img * (c1 - (gi[P + pid] * m + bg[1] * (1.f - m)));
+            dp2 += s_img * (c2 - (gi[2 * P + pid] * m + bg[2] * (1.f - m)));
+            dpa = s_a * ((1 - T_final) - m);
+        }
         if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // torch clamp gradient: passes where 0 <= x <= 1
             const unsigned m = cmask[bv * P + pid];
             dp0 = (m & 1u) ? dp0 : 0.f;
@@ -538,8 +613,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             dp2 = (m & 4u) ? dp2 : 0.f;
         }
         if (DEPTH) dpd = d_depth[bv * P + pid];
-        if (d_alpha) dpa = d_alpha[bv * P + pid];
-        cf = cfin[bv * P + pid];
+        if (d_alpha) dpa += d_alpha[bv * P + pid];
     }
     // per-pixel state entering the chunk: the forward's checkpoint (or the list head)
     float Tr = 1.0f, Dup = 0.f;
@@ -988,6 +1062,13 @@ int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, fl
                                        (unsigned char *)(ws + L.cmask), (float4 *)(ws + L.cfin),
                                        (float *)(ws + L.ck), (int2 *)(ws + L.cklist), (int *)(ws + L.nck),
                                        (unsigned *)(ws + L.misc) + 4, L.ck_region)));
+    return LGM_OK;
+}
+
+int launch_loss_reduce(const Dims &d, char *ws, const Layout &L, hipStream_t st) {
+    const double P = (double)d.H * d.W;
+    LGM_LAUNCH("k_loss_reduce", st, (k_loss_reduce<<<1, 256, 0, st>>>(d.BV * d.T, (const float *)(ws + L.lossp),
+                                                                      3.0 * d.BV * P, d.BV * P, d.loss_out)));
     return LGM_OK;
 }
 

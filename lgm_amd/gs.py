@@ -42,7 +42,8 @@ class _RasterizeBatched(torch.autograd.Function):
     """Autograd Function over all B x V renders (replaces B*V applications of the EXT _RasterizeGaussians)."""
 
     @staticmethod
-    def forward(ctx, g, cam_view, cam_view_proj, bg, tanx, tany, scale_modifier, H, W, options):
+    def forward(ctx, g, cam_view, cam_view_proj, bg, tanx, tany, scale_modifier, H, W, options, gt_img=None,
+                gt_mask=None):
         L = _native.lib()
         B, N = g.shape[0], g.shape[1]
         V = cam_view.shape[1]
@@ -65,46 +66,72 @@ class _RasterizeBatched(torch.autograd.Function):
         image = torch.empty(B, V, 3, H, W, dtype=torch.float32, device=dev)
         depth = torch.empty(B, V, 1, H, W, dtype=torch.float32, device=dev)
         alpha = torch.empty(B, V, 1, H, W, dtype=torch.float32, device=dev)
-        _native.check(L.lgm_render_forward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
-                                           _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
-                                           _native.ptr(image), _native.ptr(depth), _native.ptr(alpha), None,
-                                           _native.ptr(ws), ws_bytes, cap, None, options, stream),
-                      "lgm_render_forward")
+        if gt_img is None:
+            loss4 = torch.empty(0, dtype=torch.float32, device=dev)
+            _native.check(L.lgm_render_forward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
+                                               _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
+                                               _native.ptr(image), _native.ptr(depth), _native.ptr(alpha), None,
+                                               _native.ptr(ws), ws_bytes, cap, None, options, stream),
+                          "lgm_render_forward")
+        else:
+            # (loss_mse, mse_image, mse_alpha, psnr) of core/models.py:145-148,167, computed by the kernels
+            loss4 = torch.empty(4, dtype=torch.float32, device=dev)
+            _native.check(L.lgm_render_forward_loss(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
+                                                    _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany,
+                                                    scale_modifier, _native.ptr(image), _native.ptr(depth),
+                                                    _native.ptr(alpha), _native.ptr(gt_img), _native.ptr(gt_mask),
+                                                    _native.ptr(loss4), _native.ptr(ws), ws_bytes, cap, options,
+                                                    stream), "lgm_render_forward_loss")
         # the workspace is saved like an input: autograd frees it after a (non-retain_graph) backward, so a training
         # loop that keeps the previous step's outputs alive does not hold two workspaces
-        ctx.save_for_backward(g, cam_view, cam_view_proj, bg, ws)
+        ctx.save_for_backward(g, cam_view, cam_view_proj, bg, ws, gt_img, gt_mask, loss4)
         ctx.set_materialize_grads(False)  # unused outputs (LGM never uses depth) arrive as None, not zeros
         ctx.ws_bytes, ctx.cap = ws_bytes, cap
         ctx.params = (tanx, tany, scale_modifier, H, W, options)
         ctx.backwards = 0  # a repeated backward (retain_graph) must clear the previous one's accumulators
-        return image, depth, alpha
+        return image, depth, alpha, loss4
 
     @staticmethod
-    def backward(ctx, d_image, d_depth, d_alpha):
-        g, cam_view, cam_view_proj, bg, ws = ctx.saved_tensors
+    def backward(ctx, d_image, d_depth, d_alpha, d_loss4):
+        g, cam_view, cam_view_proj, bg, ws, gt_img, gt_mask, loss4 = ctx.saved_tensors
         tanx, tany, scale_modifier, H, W, options = ctx.params
         B, N = g.shape[0], g.shape[1]
         V = cam_view.shape[1]
-        if d_image is None:
-            d_image = torch.zeros(B, V, 3, H, W, dtype=torch.float32, device=g.device)
-        d_image = d_image.float().contiguous()
+        d_image = None if d_image is None else d_image.float().contiguous()
         d_depth = None if d_depth is None else d_depth.float().contiguous()
         d_alpha = None if d_alpha is None else d_alpha.float().contiguous()
         d_g = torch.empty_like(g)
         L = _native.lib()
         bwd_options = options | (_native.RENDER_BACKWARD_AGAIN if ctx.backwards else 0)
         ctx.backwards += 1
-        _native.check(L.lgm_render_backward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
-                                            _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
-                                            _native.ptr(d_image), _native.ptr(d_depth), _native.ptr(d_alpha),
-                                            _native.ptr(d_g), None, _native.ptr(ws), ctx.ws_bytes, ctx.cap,
-                                            bwd_options, _native.stream_of(g.device)), "lgm_render_backward")
-        return d_g, None, None, None, None, None, None, None, None, None
+        stream = _native.stream_of(g.device)
+        if gt_img is not None and d_loss4 is not None:
+            if d_depth is not None:
+                raise NotImplementedError("a depth gradient together with the fused loss (LGM's loss has no depth)")
+            # d/dmse_image of loss_mse, mse_image and psnr = -10 log10(mse_image); d/dmse_alpha of loss_mse, mse_alpha
+            d4 = d_loss4.float()
+            s2 = torch.stack([d4[0] + d4[1] - d4[3] * (10.0 / math.log(10.0)) / loss4[1], d4[0] + d4[2]]).contiguous()
+            _native.check(L.lgm_render_backward_loss(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
+                                                     _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany,
+                                                     scale_modifier, _native.ptr(d_image), _native.ptr(d_alpha),
+                                                     _native.ptr(gt_img), _native.ptr(gt_mask), _native.ptr(s2),
+                                                     _native.ptr(d_g), _native.ptr(ws), ctx.ws_bytes, ctx.cap,
+                                                     bwd_options, stream), "lgm_render_backward_loss")
+        else:
+            _native.check(L.lgm_render_backward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
+                                                _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
+                                                _native.ptr(d_image), _native.ptr(d_depth), _native.ptr(d_alpha),
+                                                _native.ptr(d_g), None, _native.ptr(ws), ctx.ws_bytes, ctx.cap,
+                                                bwd_options, stream), "lgm_render_backward")
+        return d_g, None, None, None, None, None, None, None, None, None, None, None
 
 
-def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, scale_modifier=1.0, clamp=False):
+def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, scale_modifier=1.0, clamp=False,
+              gt_images=None, gt_masks=None):
     """Functional form: returns (image [B,V,3,H,W], depth [B,V,1,H,W], alpha [B,V,1,H,W]). The image is
-    unclamped unless clamp=True, which applies core/gs.py:87's clamp(0, 1) (and its gradient) inside the kernels."""
+    unclamped unless clamp=True, which applies core/gs.py:87's clamp(0, 1) (and its gradient) inside the kernels.
+    With gt_images [B,V,3,H,W] and gt_masks [B,V,1,H,W] a 4th output (loss_mse, mse_image, mse_alpha, psnr) holds
+    LGM's training MSE terms (core/models.py:145-148,167), fused into the kernels; it is differentiable."""
     for t, n in ((gaussians, "gaussians"), (cam_view, "cam_view"), (cam_view_proj, "cam_view_proj")):
         _native.require_device_tensor(t, n)
     g = gaussians.float().contiguous()
@@ -116,8 +143,16 @@ def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, sc
         raise ValueError(f"gaussians must be [B,N,14], got {tuple(g.shape)}")
     if cv.shape[:2] != cvp.shape[:2] or cv.shape[0] != g.shape[0] or cv.shape[-2:] != (4, 4):
         raise ValueError("cam_view / cam_view_proj must be [B,V,4,4] with B matching gaussians")
-    return _RasterizeBatched.apply(g, cv, cvp, bgt, float(tanfovx), float(tanfovy), float(scale_modifier),
-                                   int(H), int(W), _native.RENDER_CLAMP_IMAGE if clamp else 0)
+    gti = gtm = None
+    if gt_images is not None or gt_masks is not None:
+        B, V = cv.shape[0], cv.shape[1]
+        gti = gt_images.to(dev, torch.float32).contiguous().detach()
+        gtm = gt_masks.to(dev, torch.float32).contiguous().detach()
+        if tuple(gti.shape) != (B, V, 3, H, W) or tuple(gtm.shape) != (B, V, 1, H, W):
+            raise ValueError("gt_images / gt_masks must be [B,V,3,H,W] / [B,V,1,H,W]")
+    out = _RasterizeBatched.apply(g, cv, cvp, bgt, float(tanfovx), float(tanfovy), float(scale_modifier),
+                                  int(H), int(W), _native.RENDER_CLAMP_IMAGE if clamp else 0, gti, gtm)
+    return out if gti is not None else out[:3]
 
 
 def count_pairs(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scale_modifier=1.0):
@@ -207,15 +242,24 @@ class GaussianRenderer:
         self.proj_matrix[3, 2] = -(opt.zfar * opt.znear) / (opt.zfar - opt.znear)
         self.proj_matrix[2, 3] = 1
 
-    def render(self, gaussians, cam_view, cam_view_proj, cam_pos, bg_color=None, scale_modifier=1):
-        # gaussians [B,N,14]; cam_view, cam_view_proj [B,V,4,4]; cam_pos [B,V,3] (unused without SH, as upstream)
+    def render(self, gaussians, cam_view, cam_view_proj, cam_pos, bg_color=None, scale_modifier=1, gt_images=None,
+               gt_masks=None):
+        """core/gs.py:31-98. gaussians [B,N,14]; cam_view, cam_view_proj [B,V,4,4]; cam_pos [B,V,3] (unused without
+        SH, as upstream). Additive: with gt_images / gt_masks (the `images_output` / `masks_output` of
+        core/models.py:140-141) the result also holds LGM's MSE loss terms, computed in the render kernels:
+        "loss_mse" (differentiable: its backward seeds the render backward in-kernel), "mse_image", "mse_alpha"
+        and "psnr" (core/models.py:145-148,165-167)."""
         S = int(self.opt.output_size)
         bg = self.bg_color if bg_color is None else bg_color
         tan = float(self.tan_half_fov)
         # core/gs.py:87's clamp(0, 1) and its gradient are applied inside the kernels
-        image, depth, alpha = rasterize(gaussians, cam_view, cam_view_proj, bg, tan, tan, S, S, scale_modifier,
-                                        clamp=True)
-        return {"image": image, "alpha": alpha, "depth": depth}
+        out = rasterize(gaussians, cam_view, cam_view_proj, bg, tan, tan, S, S, scale_modifier, clamp=True,
+                        gt_images=gt_images, gt_masks=gt_masks)
+        res = {"image": out[0], "alpha": out[2], "depth": out[1]}
+        if len(out) == 4:
+            loss4 = out[3]
+            res.update(loss_mse=loss4[0], mse_image=loss4[1], mse_alpha=loss4[2], psnr=loss4[3].detach())
+        return res
 
     def save_ply(self, gaussians, path, compatible=True):
         """core/gs.py:101-152: B == 1, prune opacity < 0.005, optionally invert activations (3DGS PLY layout)."""

@@ -530,6 +530,88 @@ __device__ void sort_oversized(unsigned long long *seg, int n, unsigned long lon
     }
 }
 
+// MSD bucket sort of one tile (the common case): ONE histogram / scan / scatter pass on the top MSD_BITS bits of
+// the tile's depth-key span (2048 buckets: ~1 entry per bucket at the typical 1.5k-entry list), then every bucket
+// is insertion-sorted on (key, id) by one thread. Exact and stable by construction (equal keys land in one bucket
+// and are ordered by id), so the result is upstream's order. Returns false -- registers and the bucket untouched --
+// when some bucket holds more than MSD_LIMIT entries (clustered depths, e.g. a flat layer facing the camera); the
+// caller then runs the LSD passes. LDS: the radix pass's per-wave counter block is reused as MSD_B u32 counters.
+#ifndef LGM_SORT_MSD
+#define LGM_SORT_MSD 1
+#endif
+constexpr int MSD_BITS = 11, MSD_B = 1 << MSD_BITS, MSD_LIMIT = 32;
+static_assert(MSD_B * 4 <= RS_WAVES * RS_B * (int)sizeof(RsCnt), "MSD counters reuse the radix counter block");
+static_assert(MSD_B % RS_THREADS == 0, "scan layout");
+
+__device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], int n, int c0, int R, int kbits, unsigned *sk, unsigned short *sp, unsigned *hc,
+                                         int *s_wsum, int *s_flag, const unsigned long long *__restrict__ seg) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int shift = kbits > MSD_BITS ? kbits - MSD_BITS : 0;
+    constexpr int BPT = MSD_B / RS_THREADS;
+    for (int q = tid; q < MSD_B; q += RS_THREADS) hc[q] = 0u;
+    if (tid == 0) *s_flag = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_MAXR; r++) {
+        const int e = c0 + r * 64 + lane;
+        if (r < R && e < n) atomicAdd(&hc[kr[r] >> shift], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of the bucket counts (BPT consecutive buckets per thread), and the largest bucket
+    unsigned loc[BPT], sum = 0u, mx = 0u;
+#pragma unroll
+    for (int j = 0; j < BPT; j++) {
+        loc[j] = hc[tid * BPT + j];
+        sum += loc[j];
+        mx = max(mx, loc[j]);
+    }
+    const int incl = wave_incl_scan((int)sum, lane);
+    if (lane == 63) s_wsum[w] = incl;
+    if (mx > (unsigned)MSD_LIMIT) *s_flag = 1;  // benign race: every writer stores 1
+    __syncthreads();
+    if (*s_flag) return false;  // workgroup-uniform
+    unsigned run = (unsigned)(incl - (int)sum);
+    for (int ww = 0; ww < w; ww++) run += (unsigned)s_wsum[ww];
+#pragma unroll
+    for (int j = 0; j < BPT; j++) {
+        hc[tid * BPT + j] = run;
+        run += loc[j];
+    }
+    __syncthreads();
+    // scatter: after it hc[b] is the END of bucket b (= the start of bucket b + 1)
+#pragma unroll
+    for (int r = 0; r < RS_MAXR; r++) {
+        const int e = c0 + r * 64 + lane;
+        if (r < R && e < n) {
+            const unsigned pos = atomicAdd(&hc[kr[r] >> shift], 1u);
+            sk[pos] = kr[r];
+            sp[pos] = (unsigned short)e;  // the entry's position in the bucket
+        }
+    }
+    __syncthreads();
+    // per-bucket insertion sort on (key, id); ids read from the bucket only for equal keys
+    for (int b = tid; b < MSD_B; b += RS_THREADS) {
+        const int lo = b ? (int)hc[b - 1] : 0, hi = (int)hc[b];
+        for (int a = lo + 1; a < hi; a++) {
+            const unsigned kv = sk[a];
+            const unsigned short pv = sp[a];
+            int z = a - 1;
+            while (z >= lo) {
+                const unsigned kz = sk[z];
+                const bool after = kz > kv || (kz == kv && (unsigned)seg[sp[z]] > (unsigned)seg[pv]);
+                if (!after) break;
+                sk[z + 1] = kz;
+                sp[z + 1] = sp[z];
+                z--;
+            }
+            sk[z + 1] = kv;
+            sp[z + 1] = pv;
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
 // One tile's bucket: LDS LSD radix sort (see the file header); all threads of the block call it.
 __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long long *__restrict__ pairs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -537,7 +619,7 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     unsigned short *sp = reinterpret_cast<unsigned short *>(sk + RS_CAP);
     RsCnt *cnt = reinterpret_cast<RsCnt *>(sp + RS_CAP);
     __shared__ unsigned s_min, s_max, s_vmax;
-    __shared__ int s_wsum[RS_WAVES], s_long;
+    __shared__ int s_wsum[RS_WAVES], s_long, s_flag;
     if (n <= 1) return;  // a single id already sits in place (low half of its key)
     unsigned long long *seg = pairs + base;
     if (n > RS_CAP) {
@@ -553,12 +635,10 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         kr[r] = 0u;
-        pr[r] = 0;
         const int e = c0 + r * 64 + lane;
         if (r < R && e < n) {
             const unsigned long long x = seg[e];
             kr[r] = (unsigned)(x >> 32);
-            pr[r] = (unsigned short)e;
             lmin = min(lmin, kr[r]);
             lmax = max(lmax, kr[r]);
             vmax = max(vmax, (unsigned)x);
@@ -569,7 +649,7 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         const int e = c0 + r * 64 + lane;
-        if (r < R && e < n) reinterpret_cast<unsigned *>(seg)[e] = (unsigned)pr[r] < n ? (unsigned)seg[0] : 0u;
+        if (r < R && e < n) reinterpret_cast<unsigned *>(seg)[e] = (unsigned)e < n ? (unsigned)seg[0] : 0u;
     }
     return;
 #endif
@@ -593,6 +673,23 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
             }
         }
     };
+    bool msd_done = false;
+#if LGM_SORT_MSD
+    if (kbits > 0)
+        msd_done = msd_sort(kr, n, c0, R, kbits, sk, sp, reinterpret_cast<unsigned *>(cnt), s_wsum, &s_flag, seg);
+#endif
+    unsigned idr[RS_MAXR];
+    if (msd_done) {  // buckets are in (key, id) order: gather the ids
+#pragma unroll
+        for (int r = 0; r < RS_MAXR; r++) {
+            idr[r] = 0u;
+            const int e = c0 + r * 64 + lane;
+            if (r < R && e < n) idr[r] = (unsigned)seg[sp[e]];
+        }
+        goto write_ids;
+    }
+#pragma unroll
+    for (int r = 0; r < RS_MAXR; r++) pr[r] = (unsigned short)(c0 + r * 64 + lane);  // bucket positions
     for (int sh = 0; sh < kbits; sh += RS_DBITS) {
         radix_pass(kr, pr, sh, min(RS_DBITS, kbits - sh), n, c0, R, sk, sp, cnt, s_wsum);
         reload();
@@ -611,7 +708,6 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     for (int q = tid + 32; q < n; q += RS_THREADS)
         if (sk[q] == sk[q - 32]) s_long = 1;
     __syncthreads();
-    unsigned idr[RS_MAXR];
     if (s_long) {
         // long runs of equal depth (e.g. a flat layer facing the camera): full LSD on (key, id) from the bucket
         // order: the id digits first (the ids themselves serve as the keys), then the depth digits
@@ -678,6 +774,7 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
             }
         }
     }
+write_ids:
     __syncthreads();  // every read of the bucket (seg) is done before the ids overwrite it in place
     unsigned *ids = reinterpret_cast<unsigned *>(seg);
 #pragma unroll

@@ -1,8 +1,8 @@
 """Fused Gaussian head (lgm_amd/head.py, include/lgm_head.h): LGM.forward_gaussians' epilogue
 (core/models.py:95-117) against its fp32 torch restatement (oracle/head_ref.py), forward and backward.
 
-Tolerances (floating point): Gaussians and all gradients (dx, d_weight, d_bias) within 1e-5 relative L2 of the
-fp32 torch restatement for fp32 input; bf16 input: the same bf16 values fed to the restatement in fp32, dx compared
+Tolerances (floating point): Gaussians and all gradients (dx, d_weight, d_bias) within max(1e-5, 2 x the fp32
+restatement's own error) relative L2 of the restatement evaluated in fp64, for fp32 input; bf16 input: the same bf16 values fed to the restatement in fp32, dx compared
 after bf16 rounding (2e-3). The kernels accumulate in a fixed order: two backward runs are bitwise identical."""
 import numpy as np
 import pytest
@@ -42,30 +42,44 @@ def test_restatement_matches_reference_semantics():
     np.testing.assert_allclose(out[..., 7:11].norm(dim=1).detach().numpy(), 1.0, rtol=1e-5)
 
 
+def _torch_ref(x, conv, d, B, V, dtype):
+    xr = x.to(dtype).clone().requires_grad_(True)
+    cr = torch.nn.Conv2d(14, 14, 1).to(dtype)
+    cr.load_state_dict({k: v.to(dtype) for k, v in conv.state_dict().items()})
+    out = forward_gaussians_epilogue(xr, cr.weight, cr.bias, B, V)
+    out.backward(d.to(dtype))
+    return {"out": out.detach().numpy(), "dx": xr.grad.numpy(), "dW": cr.weight.grad.numpy(),
+            "db": cr.bias.grad.numpy()}
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,V,h,w", [(1, 4, 64, 64), (2, 3, 17, 23), (1, 6, 160, 160), (3, 1, 1, 1)])
 def test_head_fp32_vs_torch(cuda, B, V, h, w):
+    """GPU vs the restatement evaluated in fp64, bar max(1e-5, 2 x the fp32 restatement's own error): the
+    rotation's normalisation over N Gaussians (a 153,600-term sum at cfg4) leaves torch's fp32 CPU reduction
+    ~1.4e-5 off, so the fp32 restatement cannot be the bar there."""
     x, conv, d = _inputs(B, V, h, w, seed=B * 100 + V * 10 + h)
-    xr = x.clone().requires_grad_(True)
-    cr = torch.nn.Conv2d(14, 14, 1)
-    cr.load_state_dict(conv.state_dict())
-    ref = forward_gaussians_epilogue(xr, cr.weight, cr.bias, B, V)
-    ref.backward(d)
+    r32 = _torch_ref(x, conv, d, B, V, torch.float32)
+    r64 = _torch_ref(x, conv, d, B, V, torch.float64)
     xg = x.to(cuda).requires_grad_(True)
     cg = torch.nn.Conv2d(14, 14, 1).to(cuda)
     cg.load_state_dict(conv.state_dict())
     out = gaussian_head(xg, cg, B, V)
     out.backward(d.to(cuda))
     torch.cuda.synchronize()
-    assert out.shape == ref.shape and out.dtype == torch.float32
-    assert rel_l2(out.detach().cpu().numpy(), ref.detach().numpy()) < 1e-5
-    for k, (a, b) in {"dx": (xg.grad, xr.grad), "dW": (cg.weight.grad, cr.weight.grad),
-                      "db": (cg.bias.grad, cr.bias.grad)}.items():
-        assert rel_l2(a.cpu().numpy(), b.numpy()) < 1e-5, k
-    # per-slice forward check (each activation on its own)
-    o, r = out.detach().cpu().numpy(), ref.detach().numpy()
-    for sl in (slice(0, 3), slice(3, 4), slice(4, 7), slice(7, 11), slice(11, 14)):
-        assert rel_l2(o[..., sl], r[..., sl]) < 1e-5, sl
+    assert tuple(out.shape) == r64["out"].shape and out.dtype == torch.float32
+    gpu = {"out": out.detach().cpu().numpy(), "dx": xg.grad.cpu().numpy(), "dW": cg.weight.grad.cpu().numpy(),
+           "db": cg.bias.grad.cpu().numpy()}
+
+    def check(name, a, b32, b64):
+        bar = max(1e-5, 2.0 * rel_l2(b32, b64))
+        e = rel_l2(a, b64)
+        assert e < bar, f"{name}: GPU vs fp64 {e:.3e}, bar {bar:.3e}"
+
+    for k in gpu:
+        check(k, gpu[k], r32[k], r64[k])
+    for sl in (slice(0, 3), slice(3, 4), slice(4, 7), slice(7, 11), slice(11, 14)):  # each activation on its own
+        check(f"out[{sl}]", gpu["out"][..., sl], r32["out"][..., sl], r64["out"][..., sl])
 
 
 @pytest.mark.gpu

@@ -243,13 +243,16 @@ def test_exact_count_path_matches_slot_path_512(cuda, monkeypatch):
     d_img, _, d_alpha, bg = synthetic_upstream_grads(1, V, 512, 512, seed=45)
     keep = torch.ones(1)
     outs = []
-    for budget in (None, 0):
+    for budget in (None, None, 0):
         monkeypatch.setattr(lgs, "_WS_BUDGET", budget)
         outs.append(_production(cuda, g, cv, cvp, 512, 512, bg, d_img, d_alpha, keep))
-    slot, packed = outs
+    slot, slot2, packed = outs
     for k in ("image", "alpha"):
         assert np.array_equal(slot[k], packed[k]), k
-    # same sums in a different float-atomic order: within the gradient bar of the oracle tests
+    # the same sums in a different float-atomic order: within the gradient bar (1e-4), or within 3x the
+    # run-to-run spread of the slot path itself where float-atomic ordering alone exceeds it (ill-conditioned
+    # rotation gradients of needle-like Gaussians)
     for name, sl in GROUPS.items():
+        noise = rel_l2(slot2["d_gaussians"][..., sl], slot["d_gaussians"][..., sl])
         e = rel_l2(packed["d_gaussians"][..., sl], slot["d_gaussians"][..., sl])
-        assert e < BWD_TOL, f"d_{name}: {e:.3e}"
+        assert e < max(BWD_TOL, 3.0 * noise), f"d_{name}: {e:.3e} (slot rerun spread {noise:.3e})"

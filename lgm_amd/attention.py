@@ -10,7 +10,8 @@ signatures as the reference:
 q, k and v are read in place from the packed qkv Linear output and dq/dk/dv are written back packed, so the
 reshape/unbind/permute of the reference costs no copies. fp32, bf16 and fp16 activations are supported (bf16 is
 what LGM trains with under accelerate's mixed precision); accumulation is fp32.
-No CPU path: CPU tensors raise (the xformers path of the reference is GPU-only too).
+CPU tensors (BASELINE config 1, CPU-only inference) take the torch path of lgm_amd/cpu.py, the reference's fallback
+attention (core/attention.py:51-64); GPU tensors always run the HIP kernels.
 """
 from __future__ import annotations
 
@@ -72,9 +73,13 @@ class _PackedAttention(torch.autograd.Function):
 
 
 def packed_attention(qkv: torch.Tensor, scale: float | None = None) -> torch.Tensor:
-    """qkv [B, L, 3, H, D] (the reshaped qkv Linear output) -> [B, L, H, D]; scale defaults to D^-1/2."""
+    """qkv [B, L, 3, H, D] (the reshaped qkv Linear output) -> [B, L, H, D]; scale defaults to D^-1/2.
+    GPU tensors run the HIP kernels; CPU tensors the torch path of lgm_amd/cpu.py (BASELINE config 1)."""
     if scale is None:
         scale = qkv.shape[-1] ** -0.5
+    if not qkv.is_cuda:
+        from .cpu import attention_cpu
+        return attention_cpu(qkv, scale)
     return _PackedAttention.apply(qkv, scale)
 
 

@@ -362,7 +362,9 @@ constexpr int RS_DBITS = 9, RS_B = 1 << RS_DBITS;  // digit width: a typical 26-
 #define LGM_RS_CNT16 1  // per-wave digit counters as u16 (they never exceed RS_CAP): halves their LDS
 #endif
 typedef std::conditional<LGM_RS_CNT16, unsigned short, int>::type RsCnt;
-constexpr int RS_LDS = RS_CAP * 4 + RS_CAP * 2 + RS_WAVES * RS_B * (int)sizeof(RsCnt);
+// (the MSD path below takes RS_CAP * 8 + 2048 * 4 bytes of the same block)
+constexpr int RS_LDS_LSD = RS_CAP * 4 + RS_CAP * 2 + RS_WAVES * RS_B * (int)sizeof(RsCnt);
+constexpr int RS_LDS = RS_LDS_LSD > RS_CAP * 8 + 2048 * 4 ? RS_LDS_LSD : RS_CAP * 8 + 2048 * 4;
 static_assert(RS_CAP < 65536, "u16 counters");
 static_assert(RS_LDS >= RS_CAP * 8, "sort_oversized reuses the image as u64[RS_CAP]");
 static_assert(RS_B % RS_THREADS == 0 || RS_THREADS % RS_B == 0, "bucket scan layout");
@@ -531,20 +533,23 @@ __device__ void sort_oversized(unsigned long long *seg, int n, unsigned long lon
 }
 
 // MSD bucket sort of one tile (the common case): ONE histogram / scan / scatter pass on the top MSD_BITS bits of
-// the tile's depth-key span (2048 buckets: ~1 entry per bucket at the typical 1.5k-entry list), then every bucket
-// is insertion-sorted on (key, id) by one thread. Exact and stable by construction (equal keys land in one bucket
-// and are ordered by id), so the result is upstream's order. Returns false -- registers and the bucket untouched --
-// when some bucket holds more than MSD_LIMIT entries (clustered depths, e.g. a flat layer facing the camera); the
-// caller then runs the LSD passes. LDS: the radix pass's per-wave counter block is reused as MSD_B u32 counters.
+// the tile's depth-key span (2048 buckets: ~1 entry per bucket at the typical 1.5k-entry list), then every entry
+// takes its final position = bucket start + its rank among the bucket's entries on (key, id), found by one thread
+// scanning the (few) bucket entries in LDS -- no serial insertion chains, no further passes. Exact and stable by
+// construction (equal keys share a bucket and are ranked by id), so the result is upstream's order, written as
+// ids straight into the tile's range. Returns false -- nothing written -- when some bucket holds more than
+// MSD_LIMIT entries (clustered depths, e.g. a flat layer facing the camera); the caller then runs the LSD passes.
+// LDS: keys sk [RS_CAP] u32, ids si [RS_CAP] u32, counters hc [MSD_B] u32 (40 KB: 4 workgroups per CU, as the
+// 64-VGPR cap allows anyway).
 #ifndef LGM_SORT_MSD
 #define LGM_SORT_MSD 1
 #endif
-constexpr int MSD_BITS = 11, MSD_B = 1 << MSD_BITS, MSD_LIMIT = 32;
-static_assert(MSD_B * 4 <= RS_WAVES * RS_B * (int)sizeof(RsCnt), "MSD counters reuse the radix counter block");
+constexpr int MSD_BITS = 11, MSD_B = 1 << MSD_BITS, MSD_LIMIT = 48;
 static_assert(MSD_B % RS_THREADS == 0, "scan layout");
 
-__device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], int n, int c0, int R, int kbits, unsigned *sk, unsigned short *sp, unsigned *hc,
-                                         int *s_wsum, int *s_flag, const unsigned long long *__restrict__ seg) {
+__device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const unsigned (&ir)[RS_MAXR], int n,
+                                         int c0, int R, int kbits, unsigned *sk, unsigned *si, unsigned *hc,
+                                         int *s_wsum, int *s_flag, unsigned *__restrict__ ids_out) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int shift = kbits > MSD_BITS ? kbits - MSD_BITS : 0;
     constexpr int BPT = MSD_B / RS_THREADS;
@@ -578,37 +583,28 @@ __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], int n, i
         run += loc[j];
     }
     __syncthreads();
-    // scatter: after it hc[b] is the END of bucket b (= the start of bucket b + 1)
+    // scatter (arbitrary order inside a bucket); afterwards hc[b] is the END of bucket b (= start of b + 1)
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         const int e = c0 + r * 64 + lane;
         if (r < R && e < n) {
             const unsigned pos = atomicAdd(&hc[kr[r] >> shift], 1u);
             sk[pos] = kr[r];
-            sp[pos] = (unsigned short)e;  // the entry's position in the bucket
+            si[pos] = ir[r];
         }
     }
     __syncthreads();
-    // per-bucket insertion sort on (key, id); ids read from the bucket only for equal keys
-    for (int b = tid; b < MSD_B; b += RS_THREADS) {
-        const int lo = b ? (int)hc[b - 1] : 0, hi = (int)hc[b];
-        for (int a = lo + 1; a < hi; a++) {
-            const unsigned kv = sk[a];
-            const unsigned short pv = sp[a];
-            int z = a - 1;
-            while (z >= lo) {
-                const unsigned kz = sk[z];
-                const bool after = kz > kv || (kz == kv && (unsigned)seg[sp[z]] > (unsigned)seg[pv]);
-                if (!after) break;
-                sk[z + 1] = kz;
-                sp[z + 1] = sp[z];
-                z--;
-            }
-            sk[z + 1] = kv;
-            sp[z + 1] = pv;
+    // rank inside the bucket: final position = #(bucket entries before it in (key, id) order) + bucket start
+    for (int q = tid; q < n; q += RS_THREADS) {
+        const unsigned kq = sk[q], iq = si[q], bq = kq >> shift;
+        const int lo = bq ? (int)hc[bq - 1] : 0, hi = (int)hc[bq];
+        int rank = lo;
+        for (int z = lo; z < hi; z++) {
+            const unsigned kz = sk[z];
+            rank += (kz < kq || (kz == kq && si[z] < iq)) ? 1 : 0;
         }
+        ids_out[rank] = iq;  // the bucket (read only in the load phase, before the barriers above) takes the ids
     }
-    __syncthreads();
     return true;
 }
 
@@ -629,16 +625,18 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int C = ((n + RS_THREADS - 1) / RS_THREADS) * 64;  // per-wave chunk, a multiple of 64
     const int R = C >> 6, c0 = w * C;
-    unsigned kr[RS_MAXR];
+    unsigned kr[RS_MAXR], ir[RS_MAXR];
     unsigned short pr[RS_MAXR];
     unsigned lmin = 0xffffffffu, lmax = 0u, vmax = 0u;
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         kr[r] = 0u;
+        ir[r] = 0u;
         const int e = c0 + r * 64 + lane;
         if (r < R && e < n) {
             const unsigned long long x = seg[e];
             kr[r] = (unsigned)(x >> 32);
+            ir[r] = (unsigned)x;
             lmin = min(lmin, kr[r]);
             lmax = max(lmax, kr[r]);
             vmax = max(vmax, (unsigned)x);
@@ -673,21 +671,14 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
             }
         }
     };
-    bool msd_done = false;
 #if LGM_SORT_MSD
-    if (kbits > 0)
-        msd_done = msd_sort(kr, n, c0, R, kbits, sk, sp, reinterpret_cast<unsigned *>(cnt), s_wsum, &s_flag, seg);
+    // (kr holds key - kmin: the MSD buckets split the tile's span)
+    if (kbits > 0 && msd_sort(kr, ir, n, c0, R, kbits, sk, reinterpret_cast<unsigned *>(smem) + RS_CAP,
+                              reinterpret_cast<unsigned *>(smem) + 2 * RS_CAP, s_wsum, &s_flag,
+                              reinterpret_cast<unsigned *>(seg)))
+        return;
 #endif
     unsigned idr[RS_MAXR];
-    if (msd_done) {  // buckets are in (key, id) order: gather the ids
-#pragma unroll
-        for (int r = 0; r < RS_MAXR; r++) {
-            idr[r] = 0u;
-            const int e = c0 + r * 64 + lane;
-            if (r < R && e < n) idr[r] = (unsigned)seg[sp[e]];
-        }
-        goto write_ids;
-    }
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) pr[r] = (unsigned short)(c0 + r * 64 + lane);  // bucket positions
     for (int sh = 0; sh < kbits; sh += RS_DBITS) {
@@ -774,7 +765,6 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
             }
         }
     }
-write_ids:
     __syncthreads();  // every read of the bucket (seg) is done before the ids overwrite it in place
     unsigned *ids = reinterpret_cast<unsigned *>(seg);
 #pragma unroll

@@ -132,6 +132,16 @@ def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, sc
     unclamped unless clamp=True, which applies core/gs.py:87's clamp(0, 1) (and its gradient) inside the kernels.
     With gt_images [B,V,3,H,W] and gt_masks [B,V,1,H,W] a 4th output (loss_mse, mse_image, mse_alpha, psnr) holds
     LGM's training MSE terms (core/models.py:145-148,167), fused into the kernels; it is differentiable."""
+    if not gaussians.is_cuda:  # CPU tensors: the torch path of BASELINE config 1 (lgm_amd/cpu.py), never the oracle
+        from .cpu import render_cpu
+        bgc = torch.as_tensor(bg, dtype=torch.float32).detach().cpu()
+        out = render_cpu(gaussians, cam_view.cpu(), cam_view_proj.cpu(), bgc, tanfovx, tanfovy, int(H), int(W),
+                         scale_modifier, clamp=clamp)
+        if gt_images is None and gt_masks is None:
+            return out
+        gt_c = gt_images * gt_masks + bgc.view(1, 1, 3, 1, 1) * (1 - gt_masks)  # core/models.py:145
+        mi, ma = torch.nn.functional.mse_loss(out[0], gt_c), torch.nn.functional.mse_loss(out[2], gt_masks)
+        return out + (torch.stack([mi + ma, mi, ma, -10 * torch.log10(mi)]),)
     for t, n in ((gaussians, "gaussians"), (cam_view, "cam_view"), (cam_view_proj, "cam_view_proj")):
         _native.require_device_tensor(t, n)
     g = gaussians.float().contiguous()

@@ -71,6 +71,9 @@ def gaussian_head(x: torch.Tensor, conv: nn.Conv2d, B: int, V: int) -> torch.Ten
     """x [B*V, 14, h, w] (UNet output) -> Gaussians [B, V*h*w, 14] fp32 (core/models.py:96-117)."""
     if conv.kernel_size != (1, 1) or conv.in_channels != 14 or conv.out_channels != 14 or conv.groups != 1:
         raise ValueError("conv must be nn.Conv2d(14, 14, kernel_size=1)")
+    if not x.is_cuda:  # BASELINE config 1 (CPU-only inference): torch ops, lgm_amd/cpu.py
+        from .cpu import gaussian_head_cpu
+        return gaussian_head_cpu(x, conv.weight, conv.bias, int(B), int(V))
     return _Head.apply(x, conv.weight, conv.bias, int(B), int(V))
 
 

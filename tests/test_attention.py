@@ -67,12 +67,19 @@ def test_state_dict_compatible(path):
     m.load_state_dict(params, strict=True)
 
 
-def test_cpu_tensor_fails_loudly():
-    from lgm_amd import _native
+def test_cpu_tensors_take_the_torch_path():
+    """CPU tensors (BASELINE config 1) run lgm_amd/cpu.py's torch attention, not the HIP library."""
     from lgm_amd.attention import MemEffAttention
     m = MemEffAttention(64, 2)
-    with pytest.raises(_native.NativeError):
-        m(torch.randn(1, 8, 64))
+    x = torch.randn(1, 8, 64)
+    qkv = m.qkv(x).reshape(1, 8, 3, 2, 32)
+    ref = ref_attention_core(qkv)
+    assert rel_l2(m(x).detach().numpy(), m.proj(ref).detach().numpy()) < 1e-5
+
+
+def ref_attention_core(qkv):
+    q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))
+    return ref.attention_core(q, k, v, qkv.shape[-1] ** -0.5).transpose(1, 2).reshape(qkv.shape[0], qkv.shape[1], -1)
 
 
 # ------------------------------------------------------------------------------------------------------------ GPU

@@ -30,8 +30,10 @@ def _inputs(B, V, h, w, seed, dtype=torch.float32):
 def test_module_api_cpu():
     m = GaussianHead()
     assert set(m.state_dict()) == {"conv.weight", "conv.bias"}  # LGM's self.conv (core/models.py:34)
-    with pytest.raises(_native.NativeError):
-        m(torch.randn(4, 14, 2, 2), 1, 4)  # no CPU path for the HIP head
+    x = torch.randn(4, 14, 2, 3)
+    # CPU tensors (BASELINE config 1): the torch path of lgm_amd/cpu.py
+    ref = forward_gaussians_epilogue(x, m.conv.weight, m.conv.bias, 1, 4)
+    assert rel_l2(m(x, 1, 4).detach().numpy(), ref.detach().numpy()) < 1e-6
 
 
 def test_restatement_matches_reference_semantics():

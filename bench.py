@@ -357,6 +357,11 @@ def run(args):
         result["step_roofline"] = {"bytes": step_bytes, "achieved_GBs": round(step_bytes / (ms_step / 1e3) / 1e9, 2),
                                    "frac": round(step_bytes / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}
 
+    if args.only_pool:
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        D.finalize(info)
+        return
     # ---- cfg3 with its views split over the ranks + one RCCL all-reduce of dL/dgaussians
     v0, v1 = D.shard_range(VIEWS, rank, world)
     g3 = synthetic_gaussians(1, N_GAUSS, seed=CFG3_SEED).to(dev).requires_grad_(True)
@@ -418,6 +423,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-attention", action="store_true", help="skip the secondary attention measurement")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 (LGM 'big') hot-path measurement")
+    ap.add_argument("--only-pool", action="store_true",
+                    help="only the headline workload (for counter profiles: no other kernel launches of other sizes)")
     return ap.parse_args(argv)
 
 

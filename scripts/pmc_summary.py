@@ -46,13 +46,26 @@ if "--json" in sys.argv:  # per-dispatch HBM bytes for bench.py's roofline.traff
         for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"):
             if k in m:
                 rec[k] = m[k]
+        wc = m.get("SQ_WAVE_CYCLES")
+        if wc:
+            if "SQ_WAIT_ANY" in m:
+                rec["wait_frac"] = round(m["SQ_WAIT_ANY"] / wc, 4)
+            if "SQ_ACTIVE_INST_VALU" in m:
+                rec["valu_busy_frac"] = round(m["SQ_ACTIVE_INST_VALU"] / wc, 4)
+        if m.get("SQ_LDS_IDX_ACTIVE"):
+            rec["lds_bank_conflict_frac"] = round(m.get("SQ_LDS_BANK_CONFLICT", 0.0) / m["SQ_LDS_IDX_ACTIVE"], 4)
         out[name.split("<")[0]] = rec
-    try:
-        rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
-    except OSError:
-        rev = ""
+    import os
+    rev = os.environ.get("PMC_COMMIT", "")
+    if not rev:
+        try:
+            rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+        except OSError:
+            rev = ""
     out["_meta"] = {"source": root, "commit": rev,
-                    "command": "rocprofv3 --kernel-trace --pmc <pass> -- python bench.py --steps 3 --warmup 2"}
+                    "workload": os.environ.get("PMC_WORKLOAD", "bench.py --only-pool (8-scene pool, cfg3 scenes)"),
+                    "command": "rocprofv3 --kernel-trace --pmc <pass> -- python bench.py --steps 3 --warmup 2 "
+                               "--only-pool --no-cpu-baseline"}
     path = sys.argv[sys.argv.index("--json") + 1]
     json.dump(out, open(path, "w"), indent=1)
     print("wrote", path)

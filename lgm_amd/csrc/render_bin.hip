@@ -784,7 +784,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_
                                                      const int *__restrict__ tile_count,
                                                      unsigned long long *__restrict__ pairs, int *__restrict__ order,
                                                      unsigned long long *__restrict__ counters) {
-    if (LGM_SORT_LPT == 0 && blockIdx.x == 0) {
+    if (!LGM_XCD_ORDER && LGM_SORT_LPT == 0 && blockIdx.x == 0) {
         extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
         static_assert(RS_LDS >= (ORD_BK + RS_WAVES) * 4, "order_tiles reuses the sort image");
         int *hist = reinterpret_cast<int *>(smem);
@@ -792,7 +792,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_
         return;
     }
     // LGM_SORT_LPT: k_order ran first and the sorts take their tiles longest first too
-    const int tile = LGM_SORT_LPT ? order[blockIdx.x] : (int)blockIdx.x - 1;
+    const int tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, M) : LGM_SORT_LPT ? order[blockIdx.x] : (int)blockIdx.x - 1;
     long long base;
     int n;
     tile_range(tile, slot_stride, tile_start, tile_count, base, n);
@@ -845,11 +845,11 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view,
                            cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum)));
             }
-            if (LGM_SORT_LPT) {
+            if (!LGM_XCD_ORDER && LGM_SORT_LPT) {
                 LGM_LAUNCH("k_order", st, (k_order<<<1, ORD_THREADS, 0, st>>>((int)M, L.slot ? (long long)d.N : -1LL,
                                                                              tstart, tcount, (int *)(ws + L.order))));
             }
-            LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M + (LGM_SORT_LPT ? 0 : 1), RS_THREADS, RS_LDS, st>>>(
+            LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M + (!LGM_XCD_ORDER && !LGM_SORT_LPT ? 1 : 0), RS_THREADS, RS_LDS, st>>>(
                                          (int)M, L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs,
                                          (int *)(ws + L.order), d.counters)));
         }
@@ -858,7 +858,7 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
         set_error("hipMemsetAsync failed");  // packed mode with no Gaussians: every tile range is empty
         return LGM_E_HIP;
     }
-    if (!count_only && d.N == 0) {  // the compositing kernels index their tiles through it (else: k_sort's WG 0)
+    if (!LGM_XCD_ORDER && !count_only && d.N == 0) {  // the compositing kernels index their tiles through it
         LGM_LAUNCH("k_order", st, (k_order<<<1, ORD_THREADS, 0, st>>>((int)M, L.slot ? (long long)d.N : -1LL,
                                                                      tstart, tcount, (int *)(ws + L.order))));
     }

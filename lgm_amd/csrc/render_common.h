@@ -310,6 +310,25 @@ __device__ __forceinline__ void tile_range(int tile, long long slot_stride, cons
     }
 }
 
+// XCD-grouped work order of the (view, tile) items (sort and both compositing kernels). Workgroups are dealt
+// round-robin over the 8 XCDs (MI355X_MICROARCH.md: blocks b and b + 8 share an XCD and its 4 MB L2), so block b
+// takes item xcd_item(b): the blocks of group g = b % 8 walk one contiguous eighth of the items, in (view, tile)
+// order, and neighbouring tiles -- which gather mostly the same Gaussians -- run on one L2 at about the same time.
+// (The previous LPT order dealt neighbouring tiles to all eight L2s: 5-17 % L2 hit rates in the compositing
+// kernels.) Bijective on [0, M) for any M (group sizes q + 1 for g < r, else q). Speed only, never correctness.
+#ifndef LGM_XCD_ORDER
+#define LGM_XCD_ORDER 1
+#endif
+__host__ __device__ __forceinline__ int xcd_item(int b, int M) {
+    const int q = M >> 3, r = M & 7, g = b & 7, i = b >> 3;
+    return (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + i;
+}
+__host__ __device__ __forceinline__ int xcd_group(int t, int M) {  // the block group (b % 8) that runs item t
+    const int q = M >> 3, r = M & 7;
+    return t < r * (q + 1) ? t / (q + 1) : r + (t - r * (q + 1)) / (q > 0 ? q : 1);
+}
+__host__ __device__ __forceinline__ int round8(int x) { return (x + 7) & ~7; }
+
 // Pixel of thread t inside a 16x16 tile: wavefront w owns the 8x8 quadrant (w & 1, w >> 1).
 __device__ __forceinline__ void tile_pixel(int t, int &lx, int &ly) {
     const int w = t >> 6, l = t & 63;

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
                                                     int ck_region) {
     __shared__ StageFwd S;
     __shared__ int s_ck[2];
-    const int tile = order[blockIdx.x];  // longest lists first (k_order)
+    const int tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, d.BV * d.T) : order[blockIdx.x];
     const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
     const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -273,7 +273,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     // goes to a pool slot, reserved one chunk ahead from the region's counter (thread 0), so that k_render_bwd can
     // take the chunk as a work item of its own. The pool is sharded by tile over ckctr's 8 counters; a full region
     // just leaves the rest of the tile to the previous chunk's item.
-    const int ck_reg = tile & 7;
+    // (XCD order: the region is the tile's block group and its slots are interleaved by region, so the backward's
+    // checkpoint items run on the XCD that composited the tile)
+    const int ck_reg = LGM_XCD_ORDER ? xcd_group(tile, d.BV * d.T) : (tile & 7);
     int ck_slot = -1, ck_written = 0;  // thread 0: slot reserved for the next boundary; checkpoints written
     for (int b0 = 0, c = 0; b0 < n; b0 += TILE_PIX, c++) {
         if (tid == 0) s_ck[c & 1] = ck_slot;  // reserved during chunk c - 1 (its atomic has long returned)
@@ -291,7 +293,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
             ck_slot = -1;
             if (b0 + TILE_PIX < n) {
                 const unsigned l = atomicAdd(&ckctr[ck_reg], 1u);
-                if (l < (unsigned)ck_region) ck_slot = ck_reg * ck_region + (int)l;
+                if (l < (unsigned)ck_region) ck_slot = LGM_XCD_ORDER ? (int)l * 8 + ck_reg : ck_reg * ck_region + (int)l;
             }
         }
         if (c >= 1) {
@@ -549,14 +551,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     __shared__ int sMaxLast;
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
     // ---- work item: (tile, chunk c, checkpoint slot)
-    const int M = d.BV * d.T;
+    const int M = d.BV * d.T, Mp = LGM_XCD_ORDER ? round8(M) : M;  // head items, then the checkpoint items
     int tile, c = 0, slot = -1;
     if ((int)blockIdx.x < M) {
-        tile = order[blockIdx.x];  // longest lists first (k_order)
+        tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, M) : order[blockIdx.x];
     } else {
-        slot = (int)blockIdx.x - M;
-        const int region = slot / ck_region;
-        if (slot - region * ck_region >= (int)ckctr[region]) return;  // an unused slot (workgroup-uniform)
+        if ((int)blockIdx.x < Mp) return;  // padding: the checkpoint items start at a multiple of 8
+        slot = (int)blockIdx.x - Mp;
+        const int region = LGM_XCD_ORDER ? (slot & 7) : slot / ck_region;
+        const int l = LGM_XCD_ORDER ? (slot >> 3) : slot - region * ck_region;
+        if (l >= (int)ckctr[region]) return;  // an unused slot (workgroup-uniform)
         const int2 e = cklist[slot];
         if (e.x < 0) return;  // reserved, never written
         tile = e.x;
@@ -1084,7 +1088,8 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
     }
     auto bwd = d_depth ? k_render_bwd<true> : k_render_bwd<false>;
     // work items: chunk 0 of every tile, then one per checkpoint slot (unused slots exit at once)
-    LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(d.BV * d.T + 8 * L.ck_region), 256, 0, st>>>(
+    const int M = d.BV * d.T, Mp = LGM_XCD_ORDER ? round8(M) : M;
+    LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(Mp + 8 * L.ck_region), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,

@@ -161,6 +161,11 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
     const unsigned long long lt = (1ull << lane) - 1ull;
     unsigned long long nemit = 0;  // wave-uniform
+    // The wave's flattened candidate tests. Pass 0: histogram (LDS rank per hit) + the hit list (or, without the
+    // LDS histogram, direct emission). Pass 1 (only after a hit-list overflow -- a dense batch, e.g. 512^2 views
+    // where a Gaussian covers ~10 tiles): the same tests again, each hit emitted at hbase[t] + an LDS fill rank,
+    // in parallel over the wave's candidates.
+    auto flat_tests = [&](int pass) {
     int carry = 0;
     for (int base0 = 0; base0 < total; base0 += 64) {
         sHead[tid] = -1;
@@ -189,6 +194,10 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
             t = y * d.gx + x;
         }
         const unsigned long long hm = __ballot(hit);
+        if (pass == 1) {
+            if (hit) pairs[dest(t, hbase[t] + atomicAdd(&fill[t], 1))] = srec[owner].key;
+            continue;
+        }
         nemit += __popcll(hm);
         if (!hm) continue;
         if (lds) {
@@ -210,6 +219,8 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
             if (MODE != COUNT) pairs[dest(t, pos)] = srec[owner].key;
         }
     }
+    };
+    flat_tests(0);
     if (lane == 0 && nemit) atomicAdd(&s_tot[0], nemit);
     if (lds) {
         __syncthreads();
@@ -233,18 +244,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                     pairs[dest(t, hbase[t] + sRank[h])] = srec[e2 & 511u].key;
                 }
             } else {
-                // hit list overflow (unusually dense workgroup): re-test this thread's own Gaussian's candidates
-                const BinRec &e = srec[tid];
-                const int cw = vis ? (int)e.w : 0, chh = cw ? nc / cw : 0;
-                const int cx0 = (int)(e.c0 & 0xffffu), cy0 = (int)(e.c0 >> 16);
-                for (int y = cy0; y < cy0 + chh; y++)
-                    for (int x = cx0; x < cx0 + cw; x++) {
-                        if (!ellipse_hits_rect(e.x, e.y, e.A, e.B, e.C, e.iA, e.iC, e.tau, (float)(x * BX),
-                                               (float)(x * BX + BX - 1), (float)(y * BY), (float)(y * BY + BY - 1)))
-                            continue;
-                        const int t = y * d.gx + x;
-                        pairs[dest(t, hbase[t] + atomicAdd(&fill[t], 1))] = e.key;
-                    }
+                flat_tests(1);  // hit-list overflow: the wave's tests again, emitting with LDS fill ranks
             }
         }
     }

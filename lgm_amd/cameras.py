@@ -83,3 +83,46 @@ def orbit_cameras(num_views: int, radius: float = 1.5, elevation: float = 0.0, f
 
 def tan_half_fov(fovy: float) -> float:
     return float(math.tan(0.5 * math.radians(fovy)))
+
+
+def orbit_cameras_batched(elevation, azimuth, radius: float = 1.5, fovy: float = 49.1, znear: float = 0.5,
+                          zfar: float = 2.5, device=None):
+    """Device-side batched camera build for the orbit video loops of infer.py:132-145 / app.py:
+    elevation and azimuth (degrees; scalars or [V] tensors, broadcast) -> (cam_view [V,4,4], cam_view_proj [V,4,4],
+    cam_pos [V,3]) on `device`, in one set of vectorised torch ops instead of V numpy orbit_camera calls, V
+    host->device copies and V torch.inverse calls. Same conventions as orbit_camera + cameras_from_c2w (OpenGL
+    look-at, up/forward flipped, cam_view = inverse(c2w)^T, computed in closed form for the rigid pose)."""
+    el = torch.as_tensor(elevation, dtype=torch.float32, device=device)
+    az = torch.as_tensor(azimuth, dtype=torch.float32, device=device)
+    el, az = torch.broadcast_tensors(el.reshape(-1), az.reshape(-1))
+    el, az = torch.deg2rad(el), torch.deg2rad(az)
+    campos = torch.stack([radius * torch.cos(el) * torch.sin(az), -radius * torch.sin(el),
+                          radius * torch.cos(el) * torch.cos(az)], -1)  # [V, 3], target at the origin
+    up = torch.tensor([0.0, 1.0, 0.0], device=campos.device).expand_as(campos)
+    fwd = torch.nn.functional.normalize(campos, dim=-1, eps=1e-20)
+    right = torch.nn.functional.normalize(torch.cross(up, fwd, dim=-1), dim=-1, eps=1e-20)
+    upv = torch.nn.functional.normalize(torch.cross(fwd, right, dim=-1), dim=-1, eps=1e-20)
+    R = torch.stack([right, -upv, -fwd], -1)  # columns; up and forward flipped (core/provider_lvis.py:205)
+    V = R.shape[0]
+    w2c = torch.zeros(V, 4, 4, device=campos.device)
+    w2c[:, :3, :3] = R.transpose(1, 2)
+    w2c[:, :3, 3] = -(R.transpose(1, 2) @ campos[:, :, None])[:, :, 0]
+    w2c[:, 3, 3] = 1.0
+    cam_view = w2c.transpose(1, 2)
+    cam_view_proj = cam_view @ projection_matrix(fovy, znear, zfar).to(campos.device)
+    return cam_view, cam_view_proj, -campos
+
+
+def render_orbit_frames(renderer, gaussians, azimuths, elevation: float = 0.0, radius: float = 1.5,
+                        scale_modifier: float = 1.0, chunk: int = 60):
+    """infer.py:132-145's video loop (one render per azimuth) as batched renders of `chunk` views each, with the
+    cameras built on the device: returns uint8 frames [V, H, W, 3] (on the renderer's device)."""
+    opt = renderer.opt
+    dev = gaussians.device
+    cv, cvp, cp = orbit_cameras_batched(elevation, azimuths, radius, opt.fovy, opt.znear, opt.zfar, device=dev)
+    frames = []
+    for v0 in range(0, cv.shape[0], chunk):
+        img = renderer.render(gaussians, cv[None, v0:v0 + chunk], cvp[None, v0:v0 + chunk], cp[None, v0:v0 + chunk],
+                              scale_modifier=scale_modifier)["image"][0]
+        frames.append((img.permute(0, 2, 3, 1) * 255).to(torch.uint8))
+    return torch.cat(frames, 0)

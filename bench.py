@@ -13,6 +13,8 @@ Secondary objects on the same line:
   * "cfg2": 50k Gaussians x 1 view x 256^2 forward only (BASELINE config 2), rank 0;
   * "attention": LGM's heaviest MVAttention level, bf16 fwd+bwd, MFMA and exp rooflines;
   * "cfg4": the attention blocks and the 20-view 512^2 render of one LGM 'big' forward (BASELINE config 4);
+  * "cfg5": the render side of one training step (head + 26-view 512^2 render + fused loss, fwd+bwd) and the DDP
+    gradient all-reduce of the UNet's 1.66 GB (BASELINE config 5);
   * "roofline": the dominant kernel priced with SURVEY §8(d)'s algorithmic bytes over its HIP-event time;
   * "cpu_baseline": the CPU oracle port on all host cores (rank 0, N = 1).
 
@@ -263,6 +265,55 @@ def cfg4_bench(dev, steps):
             "ms_total": round(ms_attn + ms_render, 4)}
 
 
+CFG5_VIEWS, CFG5_PARAMS = 26, 415_000_000  # rendered views per object; the 'big' UNet's parameter count
+
+
+def cfg5_bench(dev, info, steps):
+    """The render side of BASELINE config 5 (main.py:82-109 training step, one object per GPU): the fused Gaussian
+    head (core/models.py:96-117) on a synthetic UNet output of 6 input views at splat 160 (N = 153,600), the render of
+    26 views at 512^2 with the training loss fused in (core/models.py:138-148), and the backward through both; then
+    the DDP gradient exchange of the UNet's 1.66 GB fp32 gradients (100 MB buckets, bf16 on the wire:
+    lgm_amd.dist.allreduce_bucketed) -- timed on its own, since the UNet itself is out of scope."""
+    import torch
+
+    from lgm_amd import GaussianRenderer, Options
+    from lgm_amd import dist as D
+    from lgm_amd.cameras import orbit_cameras
+    from lgm_amd.head import GaussianHead
+    gen = torch.Generator().manual_seed(5)
+    head = GaussianHead().to(dev)
+    x = (torch.randn(6, 14, 160, 160, generator=gen) * 0.5).to(dev).requires_grad_(True)
+    cv, cvp, cp = (t[None].to(dev) for t in orbit_cameras(CFG5_VIEWS, elevation=-10.0))
+    gt = torch.rand(1, CFG5_VIEWS, 3, 512, 512, generator=gen).to(dev)
+    mask = (torch.rand(1, CFG5_VIEWS, 1, 512, 512, generator=gen) > 0.5).float().to(dev)
+    bg = torch.rand(3, generator=gen).to(dev)
+    r = GaussianRenderer(Options(output_size=512))
+
+    def step():
+        g = head(x, 1, 6)
+        out = r.render(g, cv, cvp, cp, bg_color=bg, gt_images=gt, gt_masks=mask)
+        out["loss_mse"].backward()
+        x.grad = None
+        head.zero_grad()
+
+    def timed(fn, n):
+        for _ in range(2):
+            fn()
+        return 1e3 * D.timed_steps(fn, n, info, torch.cuda.synchronize, dev) / n
+
+    res = {"workload": "cfg5 render side (main.py:82-109, one object per GPU): Gaussian head (6 x 160^2 -> "
+                       "153,600 Gaussians) + 26 views at 512^2 with the fused MSE loss, fwd+bwd; plus the DDP "
+                       "all-reduce of the UNet's 1.66 GB fp32 gradients (100 MB buckets, bf16 on the wire)",
+           "render_side_ms": round(timed(step, steps), 4)}
+    if info.world > 1:
+        flat = torch.zeros(CFG5_PARAMS, device=dev)
+        res["grad_allreduce_ms"] = round(timed(lambda: D.allreduce_bucketed(flat, 25_000_000, info), 3), 3)
+        del flat
+    else:
+        res["grad_allreduce_ms"] = None
+    return res
+
+
 def run(args):
     import torch
 
@@ -396,6 +447,8 @@ def run(args):
         "Mpixels_per_s": round(VIEWS * P * args.steps / el3 / 1e6, 2),
         "allreduce_ms": round(ar["ms"], 4) if world > 1 else None}
 
+    if not args.no_cfg5:  # every rank (its all-reduce is collective)
+        result["cfg5"] = cfg5_bench(dev, info, max(3, args.steps // 10))
     if rank == 0:
         result["cfg2"] = cfg2_bench(dev, args.steps)
         if not args.no_cfg4:
@@ -423,6 +476,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-attention", action="store_true", help="skip the secondary attention measurement")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 (LGM 'big') hot-path measurement")
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 (training step, render side) measurement")
     ap.add_argument("--only-pool", action="store_true",
                     help="only the headline workload (for counter profiles: no other kernel launches of other sizes)")
     return ap.parse_args(argv)

@@ -128,6 +128,13 @@ int lgm_render_debug_counters(unsigned long long *device_counters);
 #define LGM_RENDER_BACKWARD_AGAIN 4
 /* (internal) set by lgm_render_forward_loss / lgm_render_backward_loss; ignored in `options`. */
 #define LGM_RENDER_FUSED_LOSS 8
+/* LGM_RENDER_DETERMINISTIC: bit-reproducible gradients. The per-view gradient accumulators become
+ * int64 fixed point (2^-32 units; integer atomics commute, so the sums do not depend on the order in which the
+ * backward's work items finish) instead of fp32 float atomics. The forward is deterministic in either mode. The
+ * workspace is larger: size it with lgm_render_workspace_size_opts(..., options). Pass it to forward and
+ * backward alike. */
+#define LGM_RENDER_DETERMINISTIC 16
+size_t lgm_render_workspace_size_opts(int B, int V, int N, int H, int W, long long pair_capacity, int options);
 
 /* Option flags (process-wide, default 0). LGM_RENDER_NO_CULL bins upstream's full 3-sigma tile rects instead of
  * dropping (Gaussian, tile) pairs where alpha < 1/255 is provable for every pixel; outputs are identical either

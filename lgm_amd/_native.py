@@ -20,6 +20,7 @@ SIGNATURES = {
     "lgm_abi_version": (_c_int, []),
     "lgm_last_error": (ctypes.c_char_p, []),
     "lgm_render_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_ll]),
+    "lgm_render_workspace_size_opts": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_int]),
     "lgm_render_count_pairs": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_float, _c_float,
                                         _c_float, _vp, _c_size, _vp, _vp]),
     "lgm_render_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_float,
@@ -60,6 +61,7 @@ _lib = None
 ABI_VERSION = 2
 RENDER_CLAMP_IMAGE = 2  # include/lgm_render.h LGM_RENDER_CLAMP_IMAGE
 RENDER_BACKWARD_AGAIN = 4  # include/lgm_render.h LGM_RENDER_BACKWARD_AGAIN
+RENDER_DETERMINISTIC = 16  # include/lgm_render.h LGM_RENDER_DETERMINISTIC
 
 
 class NativeError(RuntimeError):

@@ -75,7 +75,7 @@ int check_ws(int B, int V, int N, int H, int W, const void *ws, size_t ws_bytes,
         lgm::set_error("invalid sizes (B=%d V=%d N=%d H=%d W=%d)", B, V, N, H, W);
         return LGM_E_INVALID;
     }
-    L = lgm::make_layout(B, V, N, H, W, cap);
+    L = lgm::make_layout(B, V, N, H, W, cap, false);
     if (!ws || ws_bytes < L.total) {
         lgm::set_error("workspace too small (%zu < %zu)", ws_bytes, L.total);
         return LGM_E_WORKSPACE;
@@ -100,6 +100,11 @@ int lgm_render_set_flags(int flags) {
 size_t lgm_render_workspace_size(int B, int V, int N, int H, int W, long long pair_capacity) {
     if (B <= 0 || V <= 0 || N < 0 || H <= 0 || W <= 0) return 0;
     return lgm::make_layout(B, V, N, H, W, pair_capacity).total;
+}
+
+size_t lgm_render_workspace_size_opts(int B, int V, int N, int H, int W, long long pair_capacity, int options) {
+    if (B <= 0 || V <= 0 || N < 0 || H <= 0 || W <= 0) return 0;
+    return lgm::make_layout(B, V, N, H, W, pair_capacity, (options & LGM_RENDER_DETERMINISTIC) != 0).total;
 }
 
 int lgm_render_count_pairs(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
@@ -138,7 +143,7 @@ static int forward_impl(int B, int V, int N, int H, int W, const float *gaussian
         lgm::set_error("null output pointer");
         return LGM_E_INVALID;
     }
-    const lgm::Layout L = lgm::make_layout(B, V, N, H, W, pair_capacity);
+    const lgm::Layout L = lgm::make_layout(B, V, N, H, W, pair_capacity, (options & LGM_RENDER_DETERMINISTIC) != 0);
     if (!L.slot && !capacity_ok(L.cap)) {  // packed tile offsets are int32; slot offsets are 64-bit
         lgm::set_error("pair capacity %lld exceeds 2^31", L.cap);
         return LGM_E_INVALID;
@@ -182,7 +187,7 @@ static int backward_impl(int B, int V, int N, int H, int W, const float *gaussia
         lgm::set_error("null pointer in backward");
         return LGM_E_INVALID;
     }
-    const lgm::Layout L = lgm::make_layout(B, V, N, H, W, pair_capacity);
+    const lgm::Layout L = lgm::make_layout(B, V, N, H, W, pair_capacity, (options & LGM_RENDER_DETERMINISTIC) != 0);
     if (!workspace || workspace_bytes < L.total) {
         lgm::set_error("workspace too small (%zu < %zu)", workspace_bytes, L.total);
         return LGM_E_WORKSPACE;

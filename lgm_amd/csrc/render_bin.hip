@@ -124,10 +124,17 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                 gP[k] = make_float4(o.x, o.y, o.A, o.B);
                 gQ[k] = make_float4(o.C, o.opacity, o.tau, o.depth);
                 rects[k] = make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16), (unsigned)o.x1 | ((unsigned)o.y1 << 16));
-                // the backward's per-view gradient accumulators start at zero (k_preproc_bwd re-zeroes them)
-                float2 *a2 = reinterpret_cast<float2 *>(accum + k * NACC);
+                // the backward's per-view gradient accumulators start at zero (a repeated backward clears them with
+                // LGM_RENDER_BACKWARD_AGAIN); int64 fixed point in deterministic mode
+                if (d.options & LGM_RENDER_DETERMINISTIC) {
+                    ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(accum) + k * (NACC / 2);
 #pragma unroll
-                for (int q = 0; q < NACC / 2; q++) a2[q] = make_float2(0.f, 0.f);
+                    for (int q = 0; q < NACC / 2; q++) a2[q] = make_ulonglong2(0ull, 0ull);
+                } else {
+                    float2 *a2 = reinterpret_cast<float2 *>(accum + k * NACC);
+#pragma unroll
+                    for (int q = 0; q < NACC / 2; q++) a2[q] = make_float2(0.f, 0.f);
+                }
             } else {
                 gP[k] = make_float4(0.f, 0.f, 0.f, 0.f);
                 gQ[k] = make_float4(0.f, 0.f, -1.f, 0.f);

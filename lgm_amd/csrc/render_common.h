@@ -17,6 +17,7 @@ constexpr int BX = 16, BY = 16, TILE_PIX = BX * BY;  // 256 pixels per tile = 4 
 constexpr int NACC = 10;                             // per-(view, Gaussian) screen-space gradient record
 constexpr int LDS_HIST_MAX = 8192;                   // tiles per view for the LDS-histogram binning path
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float DET_SCALE = 4294967296.0f;  // 2^32: deterministic-mode fixed-point units per 1.0
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -32,7 +33,9 @@ struct Layout {
     bool slot;
 };
 
-inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capacity) {
+// det (LGM_RENDER_DETERMINISTIC): the per-view gradient accumulators are int64 fixed point (2^-32 units) instead of
+// fp32: integer atomics commute, so the backward's sums do not depend on the order of its work items.
+inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capacity, bool det = false) {
     const size_t BV = (size_t)B * V, T = (size_t)((W + BX - 1) / BX) * ((H + BY - 1) / BY), P = (size_t)H * W;
     Layout L;
     L.slot = pair_capacity <= 0;
@@ -57,7 +60,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.cklist = take((size_t)8 * L.ck_region * 8);
     L.nck = take(BV * T * 4);
     L.cmask = take(BV * P);
-    L.accum = take(BV * N * NACC * 4);
+    L.accum = take(BV * N * NACC * (det ? 8 : 4));
     L.lossp = take(BV * T * 2 * 4);  // per-tile sums of squared image / alpha residuals (fused loss)
     L.total = o;
     return L;

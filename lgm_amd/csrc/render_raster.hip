@@ -908,7 +908,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const int j = f / NACC, q = f - j * NACC;
             if (q < NV && j < CH && b0 + j < s1) {
                 const float a = sAccW[0][q * LS + j];
-                if (a != 0.f) atomicAdd(accum + (gbase + reinterpret_cast<const unsigned *>(&B.R[j])[3]) * NACC + q, a);
+                const size_t ai = (gbase + reinterpret_cast<const unsigned *>(&B.R[j])[3]) * NACC + q;
+                if (a != 0.f) {
+                    if (d.options & LGM_RENDER_DETERMINISTIC)  // integer adds commute: order-independent sums
+                        atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
+                                  (unsigned long long)__float2ll_rn(a * DET_SCALE));
+                    else
+                        atomicAdd(accum + ai, a);
+                }
             }
         }
     }
@@ -949,13 +956,23 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
             if (d_means2D) { d_means2D[2 * k] = 0.f; d_means2D[2 * k + 1] = 0.f; }
             continue;
         }
-        float2 *acc2 = reinterpret_cast<float2 *>(accum + k * NACC);
         float acc[NACC];
+        if (d.options & LGM_RENDER_DETERMINISTIC) {
+            const longlong2 *acc2 = reinterpret_cast<const longlong2 *>(accum) + k * (NACC / 2);
 #pragma unroll
-        for (int q = 0; q < NACC / 2; q++) {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
-            const float2 a = acc2[q];
-            acc[2 * q] = a.x;
-            acc[2 * q + 1] = a.y;
+            for (int q = 0; q < NACC / 2; q++) {
+                const longlong2 a = acc2[q];
+                acc[2 * q] = (float)((double)a.x * (1.0 / DET_SCALE));
+                acc[2 * q + 1] = (float)((double)a.y * (1.0 / DET_SCALE));
+            }
+        } else {
+            const float2 *acc2 = reinterpret_cast<const float2 *>(accum + k * NACC);
+#pragma unroll
+            for (int q = 0; q < NACC / 2; q++) {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
+                const float2 a = acc2[q];
+                acc[2 * q] = a.x;
+                acc[2 * q + 1] = a.y;
+            }
         }
         const float dm2x = acc[0], dm2y = acc[1];
         const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
@@ -1082,7 +1099,8 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
     // the per-view accumulators were zeroed by the forward's binning; a repeated backward of the same forward
     // clears what the previous one left
     if ((d.options & LGM_RENDER_BACKWARD_AGAIN) &&
-        hipMemsetAsync(ws + L.accum, 0, (size_t)d.BV * d.N * NACC * sizeof(float), st) != hipSuccess) {
+        hipMemsetAsync(ws + L.accum, 0, (size_t)d.BV * d.N * NACC * ((d.options & LGM_RENDER_DETERMINISTIC) ? 8 : 4),
+                       st) != hipSuccess) {
         set_error("hipMemsetAsync failed");
         return LGM_E_HIP;
     }

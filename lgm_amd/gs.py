@@ -50,7 +50,7 @@ class _RasterizeBatched(torch.autograd.Function):
         dev = g.device
         stream = _native.stream_of(dev)
         cap = 0
-        ws_bytes = L.lgm_render_workspace_size(B, V, N, H, W, 0)
+        ws_bytes = L.lgm_render_workspace_size_opts(B, V, N, H, W, 0, options)
         if ws_bytes > _ws_budget(dev):
             # exact pair count (the reference syncs once per view for this; we sync once per batch)
             small = L.lgm_render_workspace_size(B, V, N, H, W, 1)
@@ -61,7 +61,7 @@ class _RasterizeBatched(torch.autograd.Function):
                                                    _native.ptr(ws), small, _native.ptr(k), stream),
                           "lgm_render_count_pairs")
             cap = max(int(k[0].item()), 1)  # pairs actually binned
-            ws_bytes = L.lgm_render_workspace_size(B, V, N, H, W, cap)
+            ws_bytes = L.lgm_render_workspace_size_opts(B, V, N, H, W, cap, options)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         image = torch.empty(B, V, 3, H, W, dtype=torch.float32, device=dev)
         depth = torch.empty(B, V, 1, H, W, dtype=torch.float32, device=dev)
@@ -126,8 +126,14 @@ class _RasterizeBatched(torch.autograd.Function):
         return d_g, None, None, None, None, None, None, None, None, None, None, None
 
 
+def deterministic_enabled() -> bool:
+    """Bit-reproducible render gradients (LGM_RENDER_DETERMINISTIC) when torch's deterministic algorithms are on
+    (torch.use_deterministic_algorithms(True)) or LGM_AMD_DETERMINISTIC=1."""
+    return torch.are_deterministic_algorithms_enabled() or os.environ.get("LGM_AMD_DETERMINISTIC", "0") == "1"
+
+
 def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, scale_modifier=1.0, clamp=False,
-              gt_images=None, gt_masks=None):
+              gt_images=None, gt_masks=None, deterministic=None):
     """Functional form: returns (image [B,V,3,H,W], depth [B,V,1,H,W], alpha [B,V,1,H,W]). The image is
     unclamped unless clamp=True, which applies core/gs.py:87's clamp(0, 1) (and its gradient) inside the kernels.
     With gt_images [B,V,3,H,W] and gt_masks [B,V,1,H,W] a 4th output (loss_mse, mse_image, mse_alpha, psnr) holds
@@ -160,8 +166,11 @@ def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, sc
         gtm = gt_masks.to(dev, torch.float32).contiguous().detach()
         if tuple(gti.shape) != (B, V, 3, H, W) or tuple(gtm.shape) != (B, V, 1, H, W):
             raise ValueError("gt_images / gt_masks must be [B,V,3,H,W] / [B,V,1,H,W]")
+    options = _native.RENDER_CLAMP_IMAGE if clamp else 0
+    if deterministic_enabled() if deterministic is None else deterministic:
+        options |= _native.RENDER_DETERMINISTIC
     out = _RasterizeBatched.apply(g, cv, cvp, bgt, float(tanfovx), float(tanfovy), float(scale_modifier),
-                                  int(H), int(W), _native.RENDER_CLAMP_IMAGE if clamp else 0, gti, gtm)
+                                  int(H), int(W), options, gti, gtm)
     return out if gti is not None else out[:3]
 
 

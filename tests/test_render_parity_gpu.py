@@ -256,3 +256,27 @@ def test_exact_count_path_matches_slot_path_512(cuda, monkeypatch):
         noise = rel_l2(slot2["d_gaussians"][..., sl], slot["d_gaussians"][..., sl])
         e = rel_l2(packed["d_gaussians"][..., sl], slot["d_gaussians"][..., sl])
         assert e < max(BWD_TOL, 3.0 * noise), f"d_{name}: {e:.3e} (slot rerun spread {noise:.3e})"
+
+
+def test_deterministic_backward(cuda, oracle_mod):
+    """LGM_RENDER_DETERMINISTIC (int64 fixed-point accumulators): two backwards of the same inputs are bitwise
+    equal, and within the gradient bar of the fp64 oracle (cfg3 with bench.py's inputs, production path)."""
+    from lgm_amd.gs import rasterize
+    g = synthetic_gaussians(1, 100_000, seed=1)
+    cv, cvp, _ = orbit_cameras(6)
+    cv, cvp = cv[None], cvp[None]
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(1, 6, 256, 256, seed=1001)
+    d_m, keep = _clamp_masked_grads(oracle_mod, g, cv, cvp, 256, 256, bg, d_img)
+    tan = TAN
+    grads = []
+    for _ in range(2):
+        gd = g.to(cuda).requires_grad_(True)
+        img, _, alp = rasterize(gd, cv.to(cuda), cvp.to(cuda), bg.to(cuda), tan, tan, 256, 256, clamp=True,
+                                deterministic=True)
+        torch.autograd.backward([img, alp], [d_img.to(cuda) * keep.to(cuda), d_alpha.to(cuda)])
+        grads.append(gd.grad.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(grads[0], grads[1])
+    out = {"image": img.detach().cpu().numpy(), "alpha": alp.detach().cpu().numpy(),
+           "d_gaussians": grads[0].cpu().numpy()}
+    _check(oracle_mod, out, g, cv, cvp, 256, 256, bg, d_m, d_alpha)

@@ -9,6 +9,8 @@
 // termination and the reverse recurrences are upstream's; exp uses v_exp_f32 (exp2 with a log2(e) prescale).
 #include "render_common.h"
 
+#include <type_traits>
+
 #ifndef LGM_BWD_BU
 #define LGM_BWD_BU 4  // backward entries evaluated per step (ILP vs registers): 1, 2 or 4
 #endif
@@ -223,6 +225,7 @@ __device__ __forceinline__ void init_sentinel(Stage &S) {
 #ifndef LGM_FWD_WPE
 #define LGM_FWD_WPE 6  // all B*V*T workgroups of the cfg3 launch are co-resident at 6 waves per SIMD (<= 80 VGPRs)
 #endif
+template <bool LOSS>  // LGM_RENDER_FUSED_LOSS compiled in (its epilogue registers stay out of the plain kernel)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE))) void k_render_fwd(Dims d, long long slot_stride, const int *__restrict__ order,
                                                     const int *__restrict__ tile_start,
                                                     const int *__restrict__ tile_count,
@@ -441,7 +444,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         out_depth[bv * P + pid] = D;
         out_alpha[bv * P + pid] = 1 - Tr;
         cfin[bv * P + pid] = make_float4(C0, C1, C2, D);  // pre-background totals for the backward
-        if (d.options & LGM_RENDER_FUSED_LOSS) {
+        if (LOSS) {
             // core/models.py:145-148: gt composited over the background, squared residuals of image and alpha
             const float m = d.gt_mask[bv * P + pid];
             const float *gi = d.gt_img + (size_t)bv * 3 * P;
@@ -453,7 +456,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
             lsq_a = ra * ra;
         }
     }
-    if (d.options & LGM_RENDER_FUSED_LOSS) {  // workgroup-uniform: per-tile partial sums, fixed order
+    if (LOSS) {  // per-tile partial sums, fixed order
         __shared__ float sL[2][4];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -530,7 +533,7 @@ __device__ __forceinline__ float row_sum16(float v) {
 #define LGM_BWD_WPE 4  // minimum waves per SIMD the register allocation must allow (4: <= 128 VGPRs; the 64-entry
                        // chunks' LDS admits 4 workgroups per CU)
 #endif
-template <bool DEPTH>
+template <bool DEPTH, bool LOSS, bool DET>  // DET: LGM_RENDER_DETERMINISTIC (int64 fixed-point flush)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 : LGM_BWD_WPE))) void k_render_bwd(
     Dims d, long long slot_stride, const int *__restrict__ order, const int *__restrict__ tile_start,
     const int *__restrict__ tile_count, const unsigned long long *__restrict__ pairs, const float4 *__restrict__ gP,
@@ -592,7 +595,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             dp1 = di[P + pid];
             dp2 = di[2 * P + pid];
         }
-        if (d.options & LGM_RENDER_FUSED_LOSS) {
+        if (LOSS) {
             // the MSE seeds (core/models.py:148): dL/dimage += 2 (image - gt) dL/dmse_image / numel, likewise alpha;
             // image recomputed from the forward's totals exactly as the forward formed it
             const float s_img = 2.f * d.d_loss[0] / (float)(3.0 * d.BV * (double)P);
@@ -910,7 +913,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 const float a = sAccW[0][q * LS + j];
                 const size_t ai = (gbase + reinterpret_cast<const unsigned *>(&B.R[j])[3]) * NACC + q;
                 if (a != 0.f) {
-                    if (d.options & LGM_RENDER_DETERMINISTIC)  // integer adds commute: order-independent sums
+                    if (DET)  // integer adds commute: order-independent sums
                         atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
                                   (unsigned long long)__float2ll_rn(a * DET_SCALE));
                     else
@@ -1074,7 +1077,8 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
 // ------------------------------------------------------------------------------------------------------------
 int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, float *image, float *depth,
                       float *alpha, char *ws, const Layout &L, hipStream_t st) {
-    LGM_LAUNCH("k_render_fwd", st, (k_render_fwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
+    auto fwd = (d.options & LGM_RENDER_FUSED_LOSS) ? k_render_fwd<true> : k_render_fwd<false>;
+    LGM_LAUNCH("k_render_fwd", st, (fwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
@@ -1104,7 +1108,13 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
         set_error("hipMemsetAsync failed");
         return LGM_E_HIP;
     }
-    auto bwd = d_depth ? k_render_bwd<true> : k_render_bwd<false>;
+    const bool loss = (d.options & LGM_RENDER_FUSED_LOSS) != 0, det = (d.options & LGM_RENDER_DETERMINISTIC) != 0;
+    auto pick = [&](auto depth_tag) {
+        constexpr bool DP = decltype(depth_tag)::value;
+        return loss ? (det ? k_render_bwd<DP, true, true> : k_render_bwd<DP, true, false>)
+                    : (det ? k_render_bwd<DP, false, true> : k_render_bwd<DP, false, false>);
+    };
+    auto bwd = d_depth ? pick(std::true_type{}) : pick(std::false_type{});
     // work items: chunk 0 of every tile, then one per checkpoint slot (unused slots exit at once)
     const int M = d.BV * d.T, Mp = LGM_XCD_ORDER ? round8(M) : M;
     LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(Mp + 8 * L.ck_region), 256, 0, st>>>(

@@ -282,7 +282,13 @@ def cfg5_bench(dev, info, steps):
     from lgm_amd.head import GaussianHead
     gen = torch.Generator().manual_seed(5)
     head = GaussianHead().to(dev)
-    x = (torch.randn(6, 14, 160, 160, generator=gen) * 0.5).to(dev).requires_grad_(True)
+    # the head's conv set so that its Gaussians follow SURVEY §8(d)'s synthetic distribution (positions 0.35 x,
+    # scales 0.1 softplus(x - 2.2522): median 0.01) rather than a random-init conv's metre-scale splats
+    with torch.no_grad():
+        head.conv.weight.copy_(torch.diag(torch.tensor([0.35] * 3 + [1.0] * 11)).view(14, 14, 1, 1))
+        head.conv.bias.zero_()
+        head.conv.bias[4:7] = -2.2522
+    x = torch.randn(6, 14, 160, 160, generator=gen).to(dev).requires_grad_(True)
     cv, cvp, cp = (t[None].to(dev) for t in orbit_cameras(CFG5_VIEWS, elevation=-10.0))
     gt = torch.rand(1, CFG5_VIEWS, 3, 512, 512, generator=gen).to(dev)
     mask = (torch.rand(1, CFG5_VIEWS, 1, 512, 512, generator=gen) > 0.5).float().to(dev)

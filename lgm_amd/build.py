@@ -40,7 +40,8 @@ def build(force: bool = False, verbose: bool = False, out: str = None, defines=(
         obj = os.path.join(HERE, "_lib", os.path.basename(src) + tag + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
                "-munsafe-fp-atomics", "-fno-slp-vectorize", "-I", os.path.join(ROOT, "include"), "-I",
-               os.path.join(HERE, "csrc"), "-c", src, "-o", obj] + [f"-D{d}" for d in defines]
+               os.path.join(HERE, "csrc"), "-c", src, "-o", obj] + \
+            [d if d.startswith("-") else f"-D{d}" for d in defines]  # A/B variants: defines or extra flags
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -103,7 +103,17 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     unsigned long long *stamp = d.counters ? d.counters + 8 + 8 * (size_t)d.BV * T +
                                              8 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x)
                                            : nullptr;
-    if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
+    // (stamps: [0] start, [1..3] the summed durations of the preprocess, tile-test and reservation phases over the
+    // batches, [4] end, [5] the last batch's hits)
+    unsigned long long t_ph = 0, ph_acc[3] = {0, 0, 0};
+    if (stamp && tid == 0) stamp[0] = t_ph = __builtin_amdgcn_s_memrealtime();
+    auto phase = [&](int k) {
+        if (stamp && tid == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            if (k >= 0) ph_acc[k] += t - t_ph;
+            t_ph = t;
+        }
+    };
     // BIN_ITERS batches of BIN_G Gaussians per workgroup, one after the other: fewer, longer workgroups fit the
     // launch into one round of residency (3 workgroups per CU by LDS)
     for (int it = 0; it < BIN_ITERS; it++) {
@@ -165,7 +175,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     const int total = __builtin_amdgcn_readlane(incl, 63);
     sExcl[tid] = excl;
     __syncthreads();  // histogram zeroed; records and exclusive offsets visible
-    if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
+    phase(0);
     const unsigned long long lt = (1ull << lane) - 1ull;
     unsigned long long nemit = 0;  // wave-uniform
     // The wave's flattened candidate tests. Pass 0: histogram (LDS rank per hit) + the hit list (or, without the
@@ -231,7 +241,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     if (lane == 0 && nemit) atomicAdd(&s_tot[0], nemit);
     if (lds) {
         __syncthreads();
-        if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
+        phase(1);
         for (int t = tid; t < T; t += BIN_THREADS) {
             const int c = hist[t];
             if (c) {
@@ -241,7 +251,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
             fill[t] = 0;
         }
         __syncthreads();
-        if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
+        phase(2);
         if (MODE != COUNT) {
             const int H = s_nhit;
             if (H <= BIN_HITCAP) {
@@ -256,8 +266,12 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         }
     }
     __syncthreads();
+    phase(-1);  // (the emit phase: the rest of the batch)
     if (stamp && tid == 0) {
-        stamp[4] = __builtin_amdgcn_s_memrealtime();
+        stamp[1] = ph_acc[0];
+        stamp[2] = ph_acc[1];
+        stamp[3] = ph_acc[2];
+        stamp[4] = t_ph;
         stamp[5] = (unsigned long long)s_nhit;
     }
     }  // batches

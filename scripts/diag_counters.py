@@ -11,22 +11,23 @@ from lgm_amd.cameras import orbit_cameras  # noqa: E402
 from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads  # noqa: E402
 
 dev = torch.device("cuda:0")
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1  # 1: cfg3 (seed 1); 8: bench.py's pool (seed 2)
 r = GaussianRenderer(Options(output_size=256))
-g = synthetic_gaussians(1, 100000, seed=1).to(dev).requires_grad_(True)
-cv, cvp, cp = orbit_cameras(6)
-d_img, _, d_alpha, bg = synthetic_upstream_grads(1, 6, 256, 256, seed=1001)
-M = 6 * 256
-NB = 6 * ((100000 + 511) // 512)  # binning records reserved (k_bin uses the first 6 * ceil(N / 1536))
+g = synthetic_gaussians(B, 100000, seed=1 if B == 1 else 2).to(dev).requires_grad_(True)
+cv, cvp, cp = (t[None].expand(B, *t.shape).contiguous().to(dev) for t in orbit_cameras(6))
+d_img, _, d_alpha, bg = synthetic_upstream_grads(B, 6, 256, 256, seed=1001 if B == 1 else 1002)
+M = B * 6 * 256
+NB = B * 6 * ((100000 + 511) // 512)  # binning records reserved (k_bin uses the first B*6*ceil(N / 1536))
 NI = 5 * M  # backward work-item capacity
 cnt = torch.zeros(8 + 8 * M + 8 * NB + 4 * NI, dtype=torch.int64, device=dev)
 L = _native.lib()
 for _ in range(5):  # warm up (clocks, caches, code objects) before the instrumented step
-    o = r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev), bg_color=bg.to(dev))
+    o = r.render(g, cv, cvp, cp, bg_color=bg.to(dev))
     torch.autograd.backward([o["image"], o["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
     g.grad = None
 torch.cuda.synchronize()
 L.lgm_render_debug_counters(_native.ptr(cnt))
-out = r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev), bg_color=bg.to(dev))
+out = r.render(g, cv, cvp, cp, bg_color=bg.to(dev))
 torch.autograd.backward([out["image"], out["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
 torch.cuda.synchronize()
 L.lgm_render_debug_counters(None)
@@ -61,7 +62,7 @@ res["fwd_lane_util"] = c[1] / max(1, 64 * c[0])
 res["bwd_lane_util"] = c[3] / max(1, 64 * c[2])
 print(json.dumps(res, indent=1))
 os.makedirs("gpurun_out", exist_ok=True)
-json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)
+json.dump(res, open(f"gpurun_out/counters_B{B}.json", "w"), indent=1)
 st, en = tl[:, 4], tl[:, 5]
 ok = en > 0
 dur = (en - st) * 0.01 if ok.any() else np.zeros(len(st))
@@ -72,21 +73,24 @@ for k in range(int(nl.max()) // 512 + 1):
         res2[f"{512 * k}-{512 * k + 511}"] = [int(m.sum()), round(float(dur[m].mean()), 2), round(float(dur[m].max()), 2)]
 print("sort us by list length [tiles, mean, max]:", json.dumps(res2))
 res["sort_us_by_n"] = res2
-json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)
+json.dump(res, open(f"gpurun_out/counters_B{B}.json", "w"), indent=1)
 
 bt = np.array(c[8 + 8 * M: 8 + 8 * M + 8 * NB], dtype=np.int64).reshape(NB, 8)
 ok = bt[:, 4] > 0
 bt = bt[ok]
 t0 = bt[:, 0].min()
-ph = {"preproc": (0, 1), "sort+tests": (1, 2), "reserve+scan": (2, 3), "emit": (3, 4), "total": (0, 4)}
-binres = {k: [round(float(np.median((bt[:, b] - bt[:, a]) * 0.01)), 2), round(float(((bt[:, b] - bt[:, a]) * 0.01).max()), 2)]
-          for k, (a, b) in ph.items()}
+# [1..3]: summed durations of the preprocess / tile-test / reservation phases over the workgroup's batches
+tot = (bt[:, 4] - bt[:, 0]) * 0.01
+phd = {"preproc": bt[:, 1] * 0.01, "tests": bt[:, 2] * 0.01, "reserve": bt[:, 3] * 0.01}
+phd["emit"] = tot - phd["preproc"] - phd["tests"] - phd["reserve"]
+phd["total"] = tot
+binres = {k: [round(float(np.median(v)), 2), round(float(v.max()), 2)] for k, v in phd.items()}
 binres["span_us"] = round(float((bt[:, 4].max() - t0) * 0.01), 2)
 binres["start_spread_us"] = round(float((bt[:, 0].max() - t0) * 0.01), 2)
 binres["hits_median"] = float(np.median(bt[:, 5]))
 print("k_bin phases [median us, max us]:", json.dumps(binres))
 res["k_bin_phases"] = binres
-json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)
+json.dump(res, open(f"gpurun_out/counters_B{B}.json", "w"), indent=1)
 
 it = np.array(c[8 + 8 * M + 8 * NB: 8 + 8 * M + 8 * NB + 4 * NI], dtype=np.int64).reshape(NI, 4)
 ok = it[:, 1] > 0
@@ -109,4 +113,4 @@ if len(it):
                       round(float((it[i, 0] - t0) * 0.01), 2)) for i in order_]
     print("bwd items:", json.dumps(ir))
     res["bwd_items"] = ir
-    json.dump(res, open("gpurun_out/counters.json", "w"), indent=1)
+    json.dump(res, open(f"gpurun_out/counters_B{B}.json", "w"), indent=1)

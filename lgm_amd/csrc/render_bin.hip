@@ -50,6 +50,9 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 #ifndef LGM_BIN_THREADS
 #define LGM_BIN_THREADS 512
 #endif
+#ifndef LGM_BIN_PREFETCH
+#define LGM_BIN_PREFETCH 1  // load batch it + 1's Gaussian rows while batch it is preprocessed and tested
+#endif
 #ifndef LGM_BIN_ITERS
 #define LGM_BIN_ITERS 3  // measured: 1 -> 50 us, 2 -> 55, 3 -> 46, 4 -> 58 (cfg3)
 #endif
@@ -115,7 +118,13 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         }
     };
     // BIN_ITERS batches of BIN_G Gaussians per workgroup, one after the other: fewer, longer workgroups fit the
-    // launch into one round of residency (3 workgroups per CU by LDS)
+    // launch into one round of residency (3 workgroups per CU by LDS). Each batch's Gaussian rows are loaded during
+    // the previous batch (registers), so only the first batch waits for its loads.
+    float gnext[14];
+    {
+        const int i0 = (blockIdx.x * BIN_ITERS) * BIN_G + tid;
+        if (i0 < d.N) load_gaussian(gauss + ((size_t)b * d.N + i0) * 14, gnext);
+    }
     for (int it = 0; it < BIN_ITERS; it++) {
     if (tid == 0) s_nhit = 0;
     if (lds)
@@ -124,9 +133,13 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     const int i = (blockIdx.x * BIN_ITERS + it) * BIN_G + tid;
     Geo o;
     bool vis = false;
+    float g[14];
+#pragma unroll
+    for (int q = 0; q < 14; q++) g[q] = gnext[q];
+    if (LGM_BIN_PREFETCH && it + 1 < BIN_ITERS && i + BIN_G < d.N)
+        load_gaussian(gauss + ((size_t)b * d.N + i + BIN_G) * 14, gnext);  // the next batch's row, in flight
     if (i < d.N) {
-        float g[14];
-        load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
+        if (!LGM_BIN_PREFETCH && it > 0) load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
         vis = preprocess_one(g, views + 16 * bv, projs + 16 * bv, d, o);
         if (MODE != COUNT) {
             const size_t k = (size_t)bv * d.N + i;

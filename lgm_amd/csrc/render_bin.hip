@@ -144,8 +144,8 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         if (MODE != COUNT) {
             const size_t k = (size_t)bv * d.N + i;
             if (vis) {
-                gP[k] = make_float4(o.x, o.y, o.A, o.B);
-                gQ[k] = make_float4(o.C, o.opacity, o.tau, o.depth);
+                gP[k] = rec_p(o.x, o.y, o.A, o.B);  // pre-scaled compositing records (render_common.h)
+                gQ[k] = rec_q(o.C, o.opacity, o.tau, o.depth);
                 rects[k] = make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16), (unsigned)o.x1 | ((unsigned)o.y1 << 16));
                 // the backward's per-view gradient accumulators start at zero (a repeated backward clears them with
                 // LGM_RENDER_BACKWARD_AGAIN); int64 fixed point in deterministic mode
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                 }
             } else {
                 gP[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-                gQ[k] = make_float4(0.f, 0.f, -1.f, 0.f);
+                gQ[k] = make_float4(0.f, -INFINITY, -1.f, 0.f);
                 rects[k] = make_uint2(0u, 0u);
             }
             if (radii_out) radii_out[k] = vis ? o.radius : 0;

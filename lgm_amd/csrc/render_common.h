@@ -195,6 +195,35 @@ __device__ __forceinline__ bool ellipse_hits_rect(float x, float y, float A, flo
     return best <= tau;
 }
 
+// Compositing records (k_bin -> k_render_fwd / k_render_bwd), two float4 per (view, Gaussian):
+//   P = (x, y, A', B'),  Q = (C', L, tau', depth)
+// with the conic pre-scaled so that one (entry, pixel) evaluation is 5 VALU + exp2:
+//   power * log2(e) + log2(opacity) = A' dx^2 + B' dx dy + C' dy^2 + L,   alpha = min(0.99, exp2(that)),
+//   A' = -KQ A, B' = -2 KQ B, C' = -KQ C (KQ = log2(e) / 2), L = log2(opacity) (-inf for opacity <= 0).
+// Upstream's `power > 0` skip is `that > L`; dL/dG = opacity dL/dalpha uses exp2(that) = opacity G directly.
+// The culling threshold tau (on q = A dx^2 + 2B dx dy + C dy^2) is stored as tau' = KQ tau, so the quadrant tests
+// run ellipse_hits_rect on (-A', -B'/2, -C', tau') = KQ (A, B, C, tau): the same test scaled by a positive constant
+// (within tau's inflation). tau >= 3e38 (never cull) is kept as is.
+constexpr float KQ = 0.5f * LOG2E;
+__device__ __forceinline__ float4 rec_p(float x, float y, float A, float B) {
+    return make_float4(x, y, -KQ * A, -LOG2E * B);
+}
+__device__ __forceinline__ float4 rec_q(float C, float opacity, float tau, float depth) {
+    return make_float4(-KQ * C, opacity > 0.f ? log2f(opacity) : -INFINITY, tau >= 3.0e38f ? tau : KQ * tau, depth);
+}
+__device__ __forceinline__ bool rec_hits_rect(const float4 &p, const float4 &q, float rx0, float rx1, float ry0,
+                                              float ry1) {
+    const float A = -p.z, B = -0.5f * p.w, C = -q.x;
+    return ellipse_hits_rect(p.x, p.y, A, B, C, 1.0f / A, 1.0f / C, q.z, rx0, rx1, ry0, ry1);
+}
+// the upstream conic and opacity back from a record (the backward's per-entry gradient conversion)
+__device__ __forceinline__ void rec_conic(const float4 &p, const float4 &q, float &A, float &B, float &C, float &op) {
+    A = p.z * (-1.0f / KQ);
+    B = p.w * (-1.0f / LOG2E);
+    C = q.x * (-1.0f / KQ);
+    op = exp2f(q.y);
+}
+
 struct Geo {
     float x, y, depth, A, B, C, opacity;  // pixel centre, view depth, conic (A, B, C), opacity
     float hx, hy;                         // half-extents of the alpha >= 1/255 ellipse's bounding box (pixels)

@@ -6,39 +6,23 @@
 // bounding box (render_common.h) against the four quadrants, and every wavefront then compacts the batch to the
 // entries that can touch its quadrant (ballot + popcount prefix), so it only iterates over Gaussians for which
 // some of its pixels pass upstream's `alpha >= 1/255` test. Per-pixel arithmetic, thresholds, the early
-// termination and the reverse recurrences are upstream's; exp uses v_exp_f32 (exp2 with a log2(e) prescale).
+// termination and the reverse recurrences are upstream's; alpha is v_exp_f32 of the pre-scaled quadratic form plus
+// log2(opacity) (the compositing records of render_common.h: 5 VALU + exp per (entry, pixel)).
 #include "render_common.h"
 
 #include <type_traits>
 
-#ifndef LGM_BWD_BU
-#define LGM_BWD_BU 4  // backward entries evaluated per step (ILP vs registers): 1, 2 or 4
-#endif
-#ifndef LGM_BWD_BRANCHY
-#define LGM_BWD_BRANCHY 0  // backward serial chain with per-lane branches (1) or as selects (0)
-#endif
 #ifndef LGM_FWD_BRANCHY
 #define LGM_FWD_BRANCHY 0  // forward serial chain with per-lane branches (1) or as selects (0)
 #endif
 #ifndef LGM_LIST_PF
 #define LGM_LIST_PF 1  // per-wave list words read one step ahead (forward)
 #endif
-#ifndef LGM_LIST_PF_BWD
-#define LGM_LIST_PF_BWD 1  // the same in the backward
-#endif
-#ifndef LGM_BWD_MASKSEL
-#define LGM_BWD_MASKSEL 1
-#endif
 #ifndef LGM_BWD_AOP_SELECT
 #define LGM_BWD_AOP_SELECT 1
 #endif
 #ifndef LGM_FWD_FU
 #define LGM_FWD_FU 4  // forward entries evaluated per step: 4 or 8
-#endif
-#ifndef LGM_BWD_MFMA
-// per-entry gradient sums as pixel moments on the MFMA: 1 = exact-f32 16x16x4, 2 = split-bf16 16x16x32 (features
-// exact in bf16, w/u as hi + lo: ~2^-16 relative per product), 0 = DPP row sums
-#define LGM_BWD_MFMA 2
 #endif
 
 namespace lgm {
@@ -61,6 +45,12 @@ __device__ __forceinline__ unsigned long long sec_stamp() {
 #define SEC_T(v)
 #define SEC_ADD(acc, a, b)
 #endif
+
+// min(0.99, e) for e = exp2(.) >= 0 as an integer min on the bits (ordered like the floats for e >= 0; NaN -> 0.99
+// as fminf): one VALU, where fminf on an exp result costs a canonicalising v_max first
+__device__ __forceinline__ float alpha_cap(float e) {
+    return __uint_as_float(min(__float_as_uint(e), 0x3f7d70a4u));
+}
 
 __device__ __forceinline__ int __reduce_add_wave(unsigned v) {
 #pragma unroll
@@ -108,7 +98,8 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #endif
 constexpr int BWD_CHUNK = LGM_BWD_CHUNK;
 static_assert(BWD_CHUNK % 64 == 0 && BWD_CHUNK <= TILE_PIX, "chunk rows");
-using StageBwd = StageT<2, 4, BWD_CHUNK>;
+// backward lists are padded to MB with the sentinel: every list position is one MFMA batch column (k_render_bwd)
+using StageBwd = StageT<2, MB, BWD_CHUNK>;
 
 // Wait for every outstanding vector-memory operation of this wave (incl. its LDS DMA). A hard s_waitcnt: the
 // compiler's waitcnt pass sees it, and does not itself track LDS written by DMA.
@@ -157,11 +148,11 @@ __device__ __forceinline__ void stage_commit(Stage &S, typename Stage::Buf &B, i
     if (have) {
         const float4 p = B.P[j], q = B.Q[j];
         if (store_id) reinterpret_cast<unsigned *>(&B.R[j])[3] = gid;
-        const float iA = 1.0f / p.z, iC = 1.0f / q.x;
+        const float A = -p.z, Bc = -0.5f * p.w, C = -q.x, iA = 1.0f / A, iC = 1.0f / C;  // KQ-scaled (render_common.h)
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const float qx = (float)(tx0 + ((k & 1) << 3)), qy = (float)(ty0 + ((k >> 1) << 3));
-            if (ellipse_hits_rect(p.x, p.y, p.z, p.w, q.x, iA, iC, q.z, qx, qx + 7.0f, qy, qy + 7.0f))
+            if (ellipse_hits_rect(p.x, p.y, A, Bc, C, iA, iC, q.z, qx, qx + 7.0f, qy, qy + 7.0f))
                 mask |= (unsigned char)(1u << k);
         }
     }
@@ -216,7 +207,7 @@ __device__ __forceinline__ void init_sentinel(Stage &S) {
     if (threadIdx.x < sizeof(S.buf) / sizeof(S.buf[0])) {
         auto &B = S.buf[threadIdx.x];
         B.P[Stage::kRows] = make_float4(0.f, 0.f, 0.f, 0.f);
-        B.Q[Stage::kRows] = make_float4(0.f, 0.f, 0.f, 0.f);
+        B.Q[Stage::kRows] = make_float4(0.f, -INFINITY, 0.f, 0.f);  // L = -inf: alpha 0
         B.R[Stage::kRows] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
@@ -356,10 +347,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
             for (int u = 0; u < FU; u++) {
                 const float4 P = Pv[u], Q = Qv[u];
                 cc[u].w = Q.w;
+                // pre-scaled records (render_common.h): lp = power log2(e) + log2(opacity), e = opacity G
                 const float dx = P.x - pfx, dy = P.y - pfy;
-                const float power = -0.5f * (P.z * dx * dx + Q.x * dy * dy) - P.w * dx * dy;
-                const float alpha = fminf(0.99f, Q.y * __builtin_amdgcn_exp2f(power * LOG2E));
-                al[u] = (power > 0.0f || alpha < 1.0f / 255.0f) ? 0.f : alpha;  // 0 == skipped
+                const float lp = fmaf(Q.x * dy, dy, fmaf(fmaf(P.w, dy, P.z * dx), dx, Q.y));
+                const float e = __builtin_amdgcn_exp2f(lp);
+                const float alpha = alpha_cap(e);
+                al[u] = (lp > Q.y || e < 1.0f / 255.0f) ? 0.f : alpha;  // 0 == skipped (power > 0 <=> lp > L)
             }
 #if LGM_FWD_BRANCHY
 #pragma unroll
@@ -525,9 +518,9 @@ __device__ __forceinline__ float row_sum16(float v) {
 // Per-entry gradient sums over a wave's 64 pixels are pixel moments on the MFMA: w = G dL/dG and u = alpha T give
 // sum_p w f(p) for f in {1, x, y, x^2, xy, y^2} (tile-centred pixel coordinates; the mean2D and conic partials
 // follow from these and the Gaussian centre) and sum_p u dL/dC_c(p): a [features x pixels] . [pixels x entries]
-// product, MB entries' w (columns 0..MB-1) and u (columns MB..) written to a per-wave LDS image and summed by
-// v_mfma_f32_16x16x32_bf16 (the geometric features are exact in bf16; w, u and dL/dC as hi + lo bf16 pairs, ~2^-16
-// relative per product). Moments are combined over the tile's four waves in LDS, turned into gradient partials per
+// product: the wave walks its list MB = 8 entries per step (list padded with the sentinel), writes their w
+// (columns 0..MB-1) and u (columns MB..) to a per-wave LDS image and sums them with v_mfma_f32_16x16x32_bf16 (the
+// geometric features are exact in bf16; w, u and dL/dC as hi + lo bf16 pairs, ~2^-16 relative per product). Moments are combined over the tile's four waves in LDS, turned into gradient partials per
 // entry and flushed once per (chunk, entry) to the per-view accumulators.
 #ifndef LGM_BWD_WPE
 #define LGM_BWD_WPE 4  // minimum waves per SIMD the register allocation must allow (4: <= 128 VGPRs; the 64-entry
@@ -647,7 +640,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const float DK = cdpf - (dpa - bg_dot) * T_final;  // Dfin - K
     const float ddelx_dx = 0.5f * d.W, ddely_dy = 0.5f * d.H;
     const size_t gbase = (size_t)bv * d.N;
-    constexpr int BU = LGM_BWD_BU;
     // MFMA operands: A (features) lane (ql, qk) holds feature ql of wave pixels 32 t + 8 qk + j, j = 0..7
     const int ql = lane & 15, qk = lane >> 4;
     const float cxT = (float)tx0 + 7.5f, cyT = (float)ty0 + 7.5f;
@@ -658,7 +650,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     for (int rr = 0; rr < 4; rr++) {
         const int row = 4 * qk + rr;
         const bool live = ql < MB ? row <= 5 : (row >= 6 && row < NV);
-        mrow[rr] = live ? row * LS : -1;  // -1: stored to the junk row
+        mrow[rr] = live ? row * LS : NV * LS;  // the junk row (all MB columns of a batch are stored)
     }
     float *myAcc = sAccW[w];
     float *myWU = sWU[w];
@@ -704,7 +696,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     int myj = 0;  // the chunk row of this lane's batch column (ql & 7)
-    auto flush_batch = [&](int nb) {
+    auto flush_batch = [&]() {
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         // B operand: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t), split hi + lo
         f32x4 a2[2];
@@ -729,9 +721,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         const f32x4 acc = a2[0] + a2[1];
         // D[row = 4 qk + r][col = ql]: moments 0..5 in the w columns, rows 6..9 in the u columns; each lane stores its
         // (at most 4) live results into this wave's slots at a per-lane row offset fixed for the kernel (mrow)
-        const bool col_ok = (ql & (MB - 1)) < nb;
 #pragma unroll
-        for (int rr = 0; rr < 4; rr++) myAcc[(col_ok && mrow[rr] >= 0) ? mrow[rr] + myj : NV * LS + lane] = acc[rr];
+        for (int rr = 0; rr < 4; rr++) myAcc[mrow[rr] + myj] = acc[rr];  // (sentinel columns: row CH, all zero)
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     };
 
@@ -763,8 +754,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             if (b0 + lane < s1 && lane < wlast - b0) {  // positions < wlast only
                 const float4 p = B.P[lane], q = B.Q[lane];
                 const float qx = (float)(tx0 + ((w & 1) << 3)), qy = (float)(ty0 + ((w >> 1) << 3));
-                hit = ellipse_hits_rect(p.x, p.y, p.z, p.w, q.x, 1.0f / p.z, 1.0f / q.x, q.z, qx, qx + 7.0f, qy,
-                                        qy + 7.0f);
+                hit = rec_hits_rect(p, q, qx, qx + 7.0f, qy, qy + 7.0f);
             }
             const unsigned long long bal = __ballot(hit);
             if (hit) S.list[w][__popcll(bal & lanemask_lt(lane))] = (unsigned short)lane;
@@ -789,88 +779,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
         const int cnt = compact_wave(S, w, lane, 0, wlast - b0);  // positions < wlast only
 #endif
-        int nb = 0;  // entries in the pending MFMA batch (wave-uniform)
-#if LGM_LIST_PF_BWD
-        static_assert(BU == 4, "the list prefetch reads whole 4-entry words");
-        uint2 lraw[1];  // the next step's list word, read one step ahead
-        list_raw<4>(S, w, 0, lraw);
-#endif
-        for (int kk = 0; kk < cnt; kk += BU) {
-            int jj4[4];
-#if LGM_LIST_PF_BWD
-            list_decode<4>(lraw, jj4);
-#else
-            list_n(S, w, kk & ~3, jj4);
-#endif
-            int jj[BU];
+        static_assert(MB == 8, "one batch = two 4-entry list words");
+        uint2 lraw[2];  // the next step's list words, read one step ahead
+        list_raw<MB>(S, w, 0, lraw);
+        for (int kk = 0; kk < cnt; kk += MB) {
+            int jj8[MB];
+            list_decode<MB>(lraw, jj8);
+            myj = S.list[w][kk + (lane & (MB - 1))];  // the entry of this lane's batch column
+            list_raw<MB>(S, w, kk + MB, lraw);        // in bounds: the list rows hold kRows + MB words
 #pragma unroll
-            for (int u = 0; u < BU; u++) jj[u] = jj4[(kk & 3) + u];
-            float al[BU], Gw[BU];
-            float4 cc[BU], Pv[BU], Qv[BU];
+            for (int h = 0; h < 2; h++) {
+                float al[4], Gw[4];
+                float4 cc[4], Pv[4], Qv[4];
 #pragma unroll
-            for (int u = 0; u < BU; u++) {  // the batch's LDS reads first, one wait (see k_render_fwd)
-                Pv[u] = B.P[jj[u]];
-                Qv[u] = B.Q[jj[u]];
-                const float4 Rj = B.R[jj[u]];
-                cc[u] = make_float4(Rj.x, Rj.y, Rj.z, 0.f);
-            }
-#if LGM_LIST_PF_BWD
-            list_raw<4>(S, w, kk + 4, lraw);  // in bounds: the list rows hold kRows + 4 words
-#endif
-            __builtin_amdgcn_sched_barrier(0);
+                for (int u = 0; u < 4; u++) {  // the LDS reads first, one wait (see k_render_fwd)
+                    const int j = jj8[4 * h + u];
+                    Pv[u] = B.P[j];
+                    Qv[u] = B.Q[j];
+                    const float4 Rj = B.R[j];
+                    cc[u] = make_float4(Rj.x, Rj.y, Rj.z, 0.f);
+                }
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int u = 0; u < BU; u++) {
-                const int pos = b0 + jj[u];  // 0-based position in the tile list
-                const float4 Pj = Pv[u], Q = Qv[u];
-                cc[u].w = Q.w;
-                const float dx = Pj.x - pfx, dy = Pj.y - pfy;
-                const float power = -0.5f * (Pj.z * dx * dx + Q.x * dy * dy) - Pj.w * dx * dy;
-                const float G = __builtin_amdgcn_exp2f(power * LOG2E);
-                const float alpha = fminf(0.99f, Q.y * G);
-                const bool ok = pos < last && power <= 0.0f && alpha >= 1.0f / 255.0f;
-                al[u] = ok ? alpha : 0.f;
-                Gw[u] = G * Q.y;  // dL/dG = opacity dL/dalpha
-            }
-            // the prefix recurrences in list order (a skipped entry, alpha 0, leaves T and D unchanged)
-            float v[BU][2];  // w = G dL/dG, u = alpha T
+                for (int u = 0; u < 4; u++) {
+                    const int pos = b0 + jj8[4 * h + u];  // 0-based position in the tile list
+                    const float4 Pj = Pv[u], Q = Qv[u];
+                    cc[u].w = Q.w;
+                    const float dx = Pj.x - pfx, dy = Pj.y - pfy;
+                    const float lp = fmaf(Q.x * dy, dy, fmaf(fmaf(Pj.w, dy, Pj.z * dx), dx, Q.y));  // as k_render_fwd
+                    const float e = __builtin_amdgcn_exp2f(lp);  // opacity G
+                    const bool ok = pos < last && lp <= Q.y && e >= 1.0f / 255.0f;
+                    al[u] = ok ? alpha_cap(e) : 0.f;
+                    Gw[u] = ok ? e : 0.f;  // dL/dG = opacity dL/dalpha (0: the entry adds nothing here)
+                }
 #pragma unroll
-            for (int u = 0; u < BU; u++) {
-                const float alpha = al[u];
-                const float4 cu = cc[u];
-                float cdp = fmaf(cu.x, dp0, fmaf(cu.y, dp1, cu.z * dp2));
-                if (DEPTH) cdp = fmaf(cu.w, dpd, cdp);
-                const float aT = alpha * Tr;
-                Dup = fmaf(aT, cdp, Dup);
-                const float om = 1.f - alpha;
-                const float r0 = __builtin_amdgcn_rcpf(om);
-                const float inv = fmaf(fmaf(-om, r0, 1.0f), r0, r0);  // 1 / (1 - alpha), ~0.5 ulp
-                const float dL_dalpha = fmaf(Tr, cdp, -(DK - Dup) * inv);
-                Tr = Tr - aT;
-#if LGM_BWD_MASKSEL
-                // a bit mask, not a select: the compiler would otherwise sink the 1/(1 - alpha) chain into an
-                // exec-masked branch that almost never skips
-                const unsigned keep = alpha != 0.f ? 0xffffffffu : 0u;
-                v[u][0] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, Gw[u] * dL_dalpha) & keep);
-#else
-                v[u][0] = alpha != 0.f ? Gw[u] * dL_dalpha : 0.f;
-#endif
-                v[u][1] = aT;  // dchannel_dcolor (0 for a skipped entry)
-            }
-#pragma unroll
-            for (int u = 0; u < BU; u++) {
-                const bool valid = al[u] != 0.f;
-                const unsigned long long bal = __ballot(valid);  // wave-uniform
-                if (bal == 0ull) continue;
-                myWU[nb * WU_LD + lane] = v[u][0];         // w
-                myWU[(MB + nb) * WU_LD + lane] = v[u][1];  // u
-                myj = (lane & (MB - 1)) == nb ? jj[u] : myj;  // the entry of batch column nb (w and u columns)
-                if (++nb == MB) {
-                    flush_batch(MB);
-                    nb = 0;
+                for (int u = 0; u < 4; u++) {  // the prefix recurrences in list order
+                    const float alpha = al[u];
+                    const float4 cu = cc[u];
+                    float cdp = fmaf(cu.x, dp0, fmaf(cu.y, dp1, cu.z * dp2));
+                    if (DEPTH) cdp = fmaf(cu.w, dpd, cdp);
+                    const float aT = alpha * Tr;
+                    Dup = fmaf(aT, cdp, Dup);
+                    const float inv = __builtin_amdgcn_rcpf(1.f - alpha);  // 1 / (1 - alpha), 1 ulp
+                    const float dL_dalpha = fmaf(Tr, cdp, -(DK - Dup) * inv);
+                    Tr = Tr - aT;
+                    myWU[(4 * h + u) * WU_LD + lane] = Gw[u] * dL_dalpha;  // w
+                    myWU[(MB + 4 * h + u) * WU_LD + lane] = aT;            // u (dchannel_dcolor)
                 }
             }
+            flush_batch();
         }
-        if (nb) flush_batch(nb);
         __syncthreads();
         // moments -> gradient partials (one thread per staged entry): the sum over the four waves' slots,
         // converted, into wave 0's slots
@@ -878,6 +836,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const int j = tid;
             const float4 Pj = B.P[j];
             const float4 Qj = B.Q[j];
+            float cA, cB, cC, op;  // the upstream conic and opacity
+            rec_conic(Pj, Qj, cA, cB, cC, op);
             const float xg = Pj.x - cxT, yg = Pj.y - cyT;
             float q[NACC];
 #pragma unroll
@@ -892,12 +852,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const float Sxy = fmaf(xg, fmaf(yg, q[0], -q[2]), fmaf(-yg, q[1], q[4]));
             const float Syy = fmaf(yg, fmaf(yg, q[0], -2.f * q[2]), q[5]);
             float *o = sAccW[0];
-            o[0 * LS + j] = -ddelx_dx * (Pj.z * Sx + Pj.w * Sy);
-            o[1 * LS + j] = -ddely_dy * (Qj.x * Sy + Pj.w * Sx);
+            o[0 * LS + j] = -ddelx_dx * (cA * Sx + cB * Sy);
+            o[1 * LS + j] = -ddely_dy * (cC * Sy + cB * Sx);
             o[2 * LS + j] = -0.5f * Sxx;
             o[3 * LS + j] = -0.5f * Sxy;
             o[4 * LS + j] = -0.5f * Syy;
-            o[5 * LS + j] = Qj.y > 0.f ? q[0] / Qj.y : 0.f;
+            o[5 * LS + j] = op > 0.f ? q[0] / op : 0.f;
 #pragma unroll
             for (int qq = 6; qq < NV; qq++) o[qq * LS + j] = q[qq];
         }

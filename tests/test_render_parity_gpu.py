@@ -224,11 +224,13 @@ def test_integer_parity_tile_lists(cuda, oracle_mod, name):
             assert np.all(ks >= 0) and np.all(np.diff(ks) > 0), f"view {v} tile {t}: not an in-order subsequence"
         nc, _, _ = oracle_mod.forward_state(g[0].numpy(), cv[0, v].numpy(), cvp[0, v].numpy(), TAN, H, H)
         nc_mismatch += int((full["n_contrib"][0, v] != nc).sum())
-    # n_contrib depends on the 1/255 and T < 1e-4 decisions, i.e. on exp(): the GPU evaluates v_exp_f32(power *
-    # log2 e), the oracle libm expf. A decision flips only where alpha lands within ~1e-7 of a threshold.
+    # n_contrib depends on the 1/255 and T < 1e-4 decisions, i.e. on exp(): the GPU evaluates
+    # v_exp_f32(A' dx^2 + B' dx dy + C' dy^2 + log2(opacity)) on the pre-scaled records (render_common.h), the
+    # oracle opacity * libm expf(power). The two agree to ~1e-6 relative in alpha, so a decision flips only where
+    # alpha lands within ~1e-6 of 1/255 (or T of 1e-4): measured 0-4 pixels of 2k-393k.
     npix = V * H * H
     print(f"{name}: n_contrib differs at {nc_mismatch} of {npix} pixels")
-    assert nc_mismatch <= max(2, npix // 100_000), f"{nc_mismatch} of {npix} pixels differ in n_contrib"
+    assert nc_mismatch <= max(4, npix // 50_000), f"{nc_mismatch} of {npix} pixels differ in n_contrib"
 
 
 def test_exact_count_path_matches_slot_path_512(cuda, monkeypatch):

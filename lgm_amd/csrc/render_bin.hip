@@ -42,11 +42,11 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 // k_bin: grid (ceil(N / BIN_G), B*V), block BIN_THREADS, one Gaussian per thread. A workgroup's LDS tile
 // histogram aggregates its BIN_G Gaussians before one global reservation per touched tile.
 //
-// Load balance: a Gaussian's work is its candidate-tile rectangle (1 to hundreds of tiles). Each wavefront
-// flattens the candidates of its 64 Gaussians into one list and tests 64 at a time (lane -> candidate; the owner
-// Gaussian found by a head-flag max-scan), so no lane idles behind a large Gaussian. Hits are recorded in an LDS
-// hit list with their rank in the tile (returned by the histogram atomic), and the emission after the global
-// reservation is a flat loop over that list.
+// Load balance: a Gaussian's work is the tile rows of its candidate rectangle (1 to tens). Each wavefront
+// flattens the rows of its 64 Gaussians into one list and takes 64 at a time (lane -> (Gaussian, row); the owner
+// Gaussian found by a head-flag max-scan), so no lane idles behind a large Gaussian; a lane computes its row's exact
+// tile range (BinRec) and records the hits in an LDS hit list with their rank in the tile (returned by the
+// histogram atomic). The emission after the global reservation is a flat loop over that list.
 #ifndef LGM_BIN_THREADS
 #define LGM_BIN_THREADS 512
 #endif
@@ -60,10 +60,19 @@ constexpr int BIN_THREADS = LGM_BIN_THREADS, BIN_G = BIN_THREADS, BIN_ITERS = LG
 constexpr int BIN_HITCAP = BIN_THREADS * 6;  // hit-list capacity (typical: ~4 hits per Gaussian)
 static_assert(BIN_THREADS <= 512, "owner index packs into 9 bits");
 
-struct BinRec {  // one Gaussian's emit record in LDS (48 B)
-    float x, y, A, B, C, iA, iC, tau;
-    unsigned c0;  // cx0 | cy0 << 16
-    unsigned w;   // candidate rect width
+// One Gaussian's emit record in LDS (48 B). The tiles a Gaussian can reach are found ROW BY ROW: for the tile row's
+// pixel band dy in [dy0, dy0 + BY - 1] the culling ellipse q = A dx^2 + 2B dx dy + C dy^2 <= tau spans
+//   x in [x - kB e' - sqrt(k0 - k1 e'^2), x - kB e + sqrt(k0 - k1 e^2)],
+//   kB = B / A, k0 = tau / A, k1 = det / A^2, e = clamp(dys, band), e' = clamp(-dys, band),
+// where dys = -B hx / C is the dy of the ellipse's rightmost point (hx = sqrt(tau C / det)): the exact x-extent of
+// (ellipse ∩ band), so the row's tiles are one contiguous range -- the same tiles as testing every candidate tile's
+// rectangle (ellipse_hits_rect), at one evaluation per row instead of per tile. Never-culled Gaussians (tau >= 3e38)
+// take k0 = inf: whole rows of the 3-sigma rect.
+struct BinRec {
+    float x, y, kB, k0, k1, dys, mg;  // mg: conservative margin (pixels) added on both sides
+    unsigned c0;                      // cx0 | cy0 << 16
+    unsigned cx1;
+    unsigned pad_;
     unsigned long long key;
 };
 
@@ -170,31 +179,39 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     unsigned long long nref = 0;
     if (vis) {
         BinRec r;
-        r.x = o.x; r.y = o.y; r.A = o.A; r.B = o.B; r.C = o.C; r.tau = o.tau;
-        r.iA = 1.0f / o.A;
-        r.iC = 1.0f / o.C;
+        r.x = o.x; r.y = o.y;
+        const float detq = o.A * o.C - o.B * o.B;
+        if (o.tau >= 3.0e38f || !(detq > 0.f) || !(o.A > 0.f) || !(o.C > 0.f)) {  // never culled: whole rows
+            r.kB = 0.f; r.k0 = INFINITY; r.k1 = 0.f; r.dys = 0.f; r.mg = 0.f;
+        } else {
+            const float iA = 1.0f / o.A;
+            r.kB = o.B * iA;
+            r.k0 = fmaxf(o.tau, 0.f) * iA;
+            r.k1 = detq * iA * iA;
+            const float hxe = sqrtf(fmaxf(o.tau, 0.f) * o.C / detq);
+            r.dys = -o.B * hxe / o.C;
+            r.mg = 1e-3f * hxe + 1e-2f;  // >> the fp32 error of the interval ends (sqrt cancellation at the edge)
+        }
         r.c0 = (unsigned)o.cx0 | ((unsigned)o.cy0 << 16);
-        r.w = (unsigned)(o.cx1 - o.cx0);
+        r.cx1 = (unsigned)o.cx1;
         r.key = ((unsigned long long)__float_as_uint(o.depth) << 32) | (unsigned)i;
         srec[tid] = r;
-        nc = (o.cx1 - o.cx0) * (o.cy1 - o.cy0);
+        nc = o.cx1 > o.cx0 ? o.cy1 - o.cy0 : 0;  // candidate tile rows
         nref = (unsigned long long)((o.x1 - o.x0) * (o.y1 - o.y0));
     }
 #pragma unroll
     for (int o2 = 32; o2 > 0; o2 >>= 1) nref += __shfl_xor(nref, o2, 64);
     if (lane == 0 && nref) atomicAdd(&s_tot[1], nref);
-    // ---- flattened exact tile tests of the wavefront's candidates
+    // ---- flattened (Gaussian, tile row) items of the wavefront: each lane finds its row's tile range
     const int incl = wave_incl_scan(nc, lane), excl = incl - nc;
     const int total = __builtin_amdgcn_readlane(incl, 63);
     sExcl[tid] = excl;
     __syncthreads();  // histogram zeroed; records and exclusive offsets visible
     phase(0);
-    const unsigned long long lt = (1ull << lane) - 1ull;
     unsigned long long nemit = 0;  // wave-uniform
-    // The wave's flattened candidate tests. Pass 0: histogram (LDS rank per hit) + the hit list (or, without the
-    // LDS histogram, direct emission). Pass 1 (only after a hit-list overflow -- a dense batch, e.g. 512^2 views
-    // where a Gaussian covers ~10 tiles): the same tests again, each hit emitted at hbase[t] + an LDS fill rank,
-    // in parallel over the wave's candidates.
+    // Pass 0: histogram (LDS rank per hit) + the hit list (or, without the LDS histogram, direct emission). Pass 1
+    // (only after a hit-list overflow -- a dense batch, e.g. 512^2 views where a Gaussian covers ~10 tiles): the
+    // same rows again, each hit emitted at hbase[t] + an LDS fill rank.
     auto flat_tests = [&](int pass) {
     int carry = 0;
     for (int base0 = 0; base0 < total; base0 += 64) {
@@ -207,46 +224,55 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         v = wave_incl_max(v, lane);
         carry = __builtin_amdgcn_readlane(v, 63);
         const int c = base0 + lane;
-        bool hit = false;
-        int t = 0, owner = 0;
+        int ta = 0, cnt = 0, trow = 0, owner = 0;
         if (c < total) {
             owner = w * 64 + v;
             const BinRec &e = srec[owner];
-            const int j = c - sExcl[owner];
-            const int cw = (int)e.w;
-            int jy = (int)((float)j * __builtin_amdgcn_rcpf((float)cw));
-            int jx = j - jy * cw;
-            if (jx < 0) { jy--; jx += cw; }
-            if (jx >= cw) { jy++; jx -= cw; }
-            const int x = (int)(e.c0 & 0xffffu) + jx, y = (int)(e.c0 >> 16) + jy;
-            hit = ellipse_hits_rect(e.x, e.y, e.A, e.B, e.C, e.iA, e.iC, e.tau, (float)(x * BX),
-                                    (float)(x * BX + BX - 1), (float)(y * BY), (float)(y * BY + BY - 1));
-            t = y * d.gx + x;
+            const int ty = (int)(e.c0 >> 16) + (c - sExcl[owner]);
+            const float dy0 = (float)(ty * BY) - e.y, dy1 = dy0 + (float)(BY - 1);
+            const float e1 = fminf(fmaxf(e.dys, dy0), dy1), e2 = fminf(fmaxf(-e.dys, dy0), dy1);
+            const float xh = e.x - e.kB * e1 + sqrtf(fmaxf(e.k0 - e.k1 * e1 * e1, 0.f)) + e.mg;
+            const float xl = e.x - e.kB * e2 - sqrtf(fmaxf(e.k0 - e.k1 * e2 * e2, 0.f)) - e.mg;
+            // tiles [BX t, BX t + BX - 1] meeting [xl, xh], within the candidate rect
+            const int cx0 = (int)(e.c0 & 0xffffu), cx1 = (int)e.cx1;
+            const float fa = ceilf((xl - (float)(BX - 1)) * (1.0f / BX)), fb = floorf(xh * (1.0f / BX)) + 1.f;
+            ta = (int)fminf(fmaxf(fa, (float)cx0), (float)cx1);  // (float clamps: +-inf and NaN safe)
+            const int tb = (int)fminf(fmaxf(fb, (float)ta), (float)cx1);
+            cnt = tb - ta;
+            trow = ty * d.gx;
         }
-        const unsigned long long hm = __ballot(hit);
         if (pass == 1) {
-            if (hit) pairs[dest(t, hbase[t] + atomicAdd(&fill[t], 1))] = srec[owner].key;
+            for (int k = 0; k < cnt; k++) {
+                const int t = trow + ta + k;
+                pairs[dest(t, hbase[t] + atomicAdd(&fill[t], 1))] = srec[owner].key;
+            }
             continue;
         }
-        nemit += __popcll(hm);
-        if (!hm) continue;
+        const int hincl = wave_incl_scan(cnt, lane);
+        const int htot = __builtin_amdgcn_readlane(hincl, 63);
+        nemit += (unsigned)htot;
+        if (!htot) continue;
         if (lds) {
             int slot0 = 0;
-            if (MODE != COUNT && lane == 0) slot0 = atomicAdd(&s_nhit, __popcll(hm));
-            slot0 = __builtin_amdgcn_readlane(slot0, 0);
-            if (hit) {
+            if (MODE != COUNT && lane == 0) slot0 = atomicAdd(&s_nhit, htot);
+            slot0 = __builtin_amdgcn_readlane(slot0, 0) + hincl - cnt;
+            for (int k = 0; k < cnt; k++) {
+                const int t = trow + ta + k;
                 const int rk = atomicAdd(&hist[t], 1);
                 if (MODE != COUNT) {
-                    const int slot = slot0 + __popcll(hm & lt);
+                    const int slot = slot0 + k;
                     if (slot < BIN_HITCAP) {
                         sHit[slot] = (unsigned)owner | ((unsigned)t << 9);
                         sRank[slot] = (unsigned short)rk;
                     }
                 }
             }
-        } else if (hit) {
-            const int pos = atomicAdd(&cur[t], 1);
-            if (MODE != COUNT) pairs[dest(t, pos)] = srec[owner].key;
+        } else {
+            for (int k = 0; k < cnt; k++) {
+                const int t = trow + ta + k;
+                const int pos = atomicAdd(&cur[t], 1);
+                if (MODE != COUNT) pairs[dest(t, pos)] = srec[owner].key;
+            }
         }
     }
     };

@@ -26,8 +26,8 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 //   slot mode   (pair_capacity <= 0): tile (bv, t) owns pairs[(bv*T + t) * N, +N): no counting pass, no scan.
 //   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
 struct Layout {
-    size_t gP, gQ, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, cfin, ck, cklist, nck, cmask, accum,
-        lossp, misc, total;
+    size_t gP, gQ, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, wlast, cfin, ck, cklist, nck, cmask,
+        accum, lossp, misc, total;
     long long cap;
     int ck_region;  // backward checkpoint slots per region (8 regions; the forward shards tiles over them)
     bool slot;
@@ -53,6 +53,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.pairs = take((size_t)L.cap * 8);
     L.final_T = take(BV * P * 4);
     L.n_contrib = take(BV * P * 4);
+    L.wlast = take(BV * T * 16);  // per tile: the four waves' largest last contributor (forward -> backward)
     L.cfin = take(BV * P * 16);  // per-pixel pre-background colour and depth totals (forward -> backward)
     // backward checkpoints (k_render_fwd -> k_render_bwd): 2 per tile on average, 5 planes of 256 floats each
     L.ck_region = (int)((2 * BV * T + 7) / 8);

@@ -12,14 +12,8 @@
 
 #include <type_traits>
 
-#ifndef LGM_FWD_BRANCHY
-#define LGM_FWD_BRANCHY 0  // forward serial chain with per-lane branches (1) or as selects (0)
-#endif
 #ifndef LGM_LIST_PF
 #define LGM_LIST_PF 1  // per-wave list words read one step ahead (forward)
-#endif
-#ifndef LGM_BWD_AOP_SELECT
-#define LGM_BWD_AOP_SELECT 1
 #endif
 #ifndef LGM_FWD_FU
 #define LGM_FWD_FU 4  // forward entries evaluated per step: 4 or 8
@@ -226,6 +220,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
                                                     const float *__restrict__ bg, float *__restrict__ out_img,
                                                     float *__restrict__ out_depth, float *__restrict__ out_alpha,
                                                     float *__restrict__ final_T, int *__restrict__ n_contrib,
+                                                    int *__restrict__ wlast_out,
                                                     unsigned char *__restrict__ cmask, float4 *__restrict__ cfin,
                                                     float *__restrict__ ck, int2 *__restrict__ cklist,
                                                     int *__restrict__ nck, unsigned *__restrict__ ckctr,
@@ -248,8 +243,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     const size_t gbase = (size_t)bv * d.N;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     init_sentinel(S);
-    bool done = !inside;
-    float Tr = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
+    // Tr < 0 marks a saturated pixel (|Tr| its final transmittance): outside pixels start saturated
+    float Tr = inside ? 1.0f : -1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     int last = 0;
     constexpr int FU = LGM_FWD_FU;
     unsigned c_iter = 0, c_acc = 0, c_list = 0;  // diagnostic work counters (Dims::counters)
@@ -273,7 +268,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     int ck_slot = -1, ck_written = 0;  // thread 0: slot reserved for the next boundary; checkpoints written
     for (int b0 = 0, c = 0; b0 < n; b0 += TILE_PIX, c++) {
         if (tid == 0) s_ck[c & 1] = ck_slot;  // reserved during chunk c - 1 (its atomic has long returned)
-        if (__syncthreads_count(done) == TILE_PIX) break;  // also: every wave is done with the previous chunk
+        if (__syncthreads_count(Tr < 0.f) == TILE_PIX) break;  // also: every wave is done with the previous chunk
         c_list += min(TILE_PIX, n - b0);
         const int k = b0 + tid;
         StageBuf &B = S.buf[cur];
@@ -294,7 +289,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
             const int sl = s_ck[c & 1];  // workgroup-uniform
             if (sl >= 0) {
                 float *cp = ck + (size_t)sl * 5 * TILE_PIX;
-                cp[tid] = Tr;
+                cp[tid] = fabsf(Tr);
                 cp[TILE_PIX + tid] = C0;
                 cp[2 * TILE_PIX + tid] = C1;
                 cp[3 * TILE_PIX + tid] = C2;
@@ -320,7 +315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         list_raw<FU>(S, w, 0, lraw);
 #endif
         for (int kk = 0; kk < cnt; kk += FU) {
-            if (__ballot(!done) == 0ull) break;
+            if (__ballot(Tr > 0.f) == 0ull) break;
             c_iter += min(FU, cnt - kk);
             int jj[FU];
 #if LGM_LIST_PF
@@ -354,52 +349,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
                 const float alpha = alpha_cap(e);
                 al[u] = (lp > Q.y || e < 1.0f / 255.0f) ? 0.f : alpha;  // 0 == skipped (power > 0 <=> lp > L)
             }
-#if LGM_FWD_BRANCHY
-#pragma unroll
-            for (int u = 0; u < FU; u++) {
-                if (done || al[u] == 0.f) continue;
-                const float alpha = al[u];
-                const float test_T = Tr * (1 - alpha);
-                if (test_T < 0.0001f) {
-                    done = true;
-                    continue;
-                }
-                C0 += cc[u].x * alpha * Tr;
-                C1 += cc[u].y * alpha * Tr;
-                C2 += cc[u].z * alpha * Tr;
-                D += cc[u].w * alpha * Tr;
-                Tr = test_T;
-                last = b0 + jj[u] + 1;
-                c_acc++;
-            }
-#else
-            // the serial chain as selects: no per-lane branches for the compiler to sink the alpha evaluations
-            // into, so the FU evaluations above stay independent (ILP across the exp latencies)
+            // the serial chain as selects (no per-lane branches for the compiler to sink the alpha evaluations into,
+            // so the FU evaluations above stay independent): upstream's test_T = T (1 - alpha) and T < 1e-4
+            // termination, with the termination kept in Tr's sign -- a skipped entry (alpha 0) leaves test_T = T,
+            // a saturated pixel (Tr < 0) has test_T <= 0, so one compare decides both
 #pragma unroll
             for (int u = 0; u < FU; u++) {
                 const float alpha = al[u];
                 const float test_T = Tr * (1 - alpha);
-                const bool live = !done && alpha != 0.f;
-                const bool acc = live && test_T >= 0.0001f;
-                done = done || (live && !acc);
-                const float aw = acc ? alpha * Tr : 0.f;
+                const bool keep = test_T >= 0.0001f;
+                const float aw = keep ? alpha * Tr : 0.f;
                 C0 = fmaf(cc[u].x, aw, C0);
                 C1 = fmaf(cc[u].y, aw, C1);
                 C2 = fmaf(cc[u].z, aw, C2);
                 D = fmaf(cc[u].w, aw, D);
-                Tr = acc ? test_T : Tr;
+                Tr = keep ? test_T : -fabsf(Tr);
+                const bool acc = keep && alpha != 0.f;
                 last = acc ? b0 + jj[u] + 1 : last;
 #ifdef LGM_WORK_COUNTERS
                 c_acc += acc ? 1u : 0u;
 #endif
             }
-#endif
         }
     }
     if (LGM_FWD_DB != 0 && pre) vm_wait_all();  // no LDS DMA may be in flight when the workgroup retires
     if (tid == 0) {
         if (ck_slot >= 0) cklist[ck_slot] = make_int2(-1, 0);  // reserved for a boundary never reached
         nck[tile] = ck_written;  // checkpoints c = 1 .. ck_written exist (a prefix: the counters only grow)
+    }
+    {  // the wave's largest last contributor (outside pixels: 0), for the backward's list bounds
+        const int wl = wave_max_i32(last);
+        if (lane == 0) wlast_out[4 * (size_t)tile + w] = wl;
     }
     if (d.counters) {
         c_acc = (unsigned)__reduce_add_wave(c_acc);
@@ -417,6 +397,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     }
     float lsq_img = 0.f, lsq_a = 0.f;  // fused loss: this pixel's squared residuals
     if (inside) {
+        Tr = fabsf(Tr);  // (the sign only marked saturation)
         const size_t P = (size_t)d.H * d.W;
         const size_t pid = (size_t)d.W * py + px;
         final_T[bv * P + pid] = Tr;
@@ -531,8 +512,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     Dims d, long long slot_stride, const int *__restrict__ order, const int *__restrict__ tile_start,
     const int *__restrict__ tile_count, const unsigned long long *__restrict__ pairs, const float4 *__restrict__ gP,
     const float4 *__restrict__ gQ, const float *__restrict__ gauss, const float *__restrict__ bg,
-    const float *__restrict__ final_T, const int *__restrict__ n_contrib, const float4 *__restrict__ cfin,
-    const float *__restrict__ ck, const int2 *__restrict__ cklist, const int *__restrict__ nck,
+    const float *__restrict__ final_T, const int *__restrict__ n_contrib, const int *__restrict__ wlast_fwd,
+    const float4 *__restrict__ cfin, const float *__restrict__ ck, const int2 *__restrict__ cklist,
+    const int *__restrict__ nck,
     const unsigned *__restrict__ ckctr, int ck_region, const float *__restrict__ d_img,
     const float *__restrict__ d_depth, const float *__restrict__ d_alpha, const unsigned char *__restrict__ cmask,
     float *__restrict__ accum, long long item_stamps) {
@@ -544,7 +526,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // (row NV of each wave's slot is a junk row: the MFMA results a lane does not keep are stored there, so the
     // stores need no exec-masked branches)
     __shared__ __attribute__((aligned(16))) float sAccW[4][LS * (NV + 1)];
-    __shared__ int sMaxLast;
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
     // ---- work item: (tile, chunk c, checkpoint slot)
     const int M = d.BV * d.T, Mp = LGM_XCD_ORDER ? round8(M) : M;  // head items, then the checkpoint items
@@ -623,13 +604,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         Dup = fmaf(cp[TILE_PIX + tid], dp0, fmaf(cp[2 * TILE_PIX + tid], dp1, cp[3 * TILE_PIX + tid] * dp2));
         if (DEPTH) Dup = fmaf(cp[4 * TILE_PIX + tid], dpd, Dup);
     }
-    init_sentinel(S);
-    if (tid == 0) sMaxLast = 0;
-    __syncthreads();
-    const int wlast = wave_max_i32(last);  // positions >= wlast touch no pixel of this wave
-    if (lane == 0 && wlast > 0) atomicMax(&sMaxLast, wlast);
-    __syncthreads();
-    const int nlist = min(n, sMaxLast);  // entries behind every pixel's last contributor are never visited
+    init_sentinel(S);  // (published by the first barrier of the chunk loop)
+    // the forward's per-wave maxima of the last contributors: positions >= wlast touch no pixel of this wave, and
+    // entries behind every pixel's last contributor are never visited
+    const int4 wl4 = reinterpret_cast<const int4 *>(wlast_fwd)[tile];
+    const int wlast = w == 0 ? wl4.x : w == 1 ? wl4.y : w == 2 ? wl4.z : wl4.w;
+    const int nlist = min(n, max(max(wl4.x, wl4.y), max(wl4.z, wl4.w)));
     const int s0 = c * TILE_PIX;
     if (s0 >= nlist) return;  // workgroup-uniform
     const int s1 = (c + 1 <= nck[tile]) ? min(nlist, s0 + TILE_PIX) : nlist;
@@ -659,39 +639,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     myWU[128 + lane] = dp2;
     myWU[192 + lane] = dpd;
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // A operand: lane (ql, qk) holds feature ql at the wave pixels p = 32 t2 + 8 qk + j, j = 0..7, i.e. tile-centred
+    // fx = fx0 + j and fy = fy0 + 4 t2 + qk: the geometric features (rows 0..5) are a + b j + c j^2 with per-lane
+    // coefficients, exact in bf16 (small integers and halves); rows 6..9 are dL/dpixel, split hi + lo.
     bf16x8 Ah[2], Al[2];
+    {
+        const float fx0 = (float)((w & 1) << 3) - 7.5f, fy0 = (float)((w >> 1) << 3) - 7.5f;
+        const int qd = min(max(ql - 6, 0), 3);  // the dL/dpixel row of lanes 6..9
 #pragma unroll
-    for (int t2 = 0; t2 < 2; t2++) {
+        for (int t2 = 0; t2 < 2; t2++) {
+            const float fy = fy0 + (float)(4 * t2 + qk);
+            const float ca = ql == 0 ? 1.f : ql == 1 ? fx0 : ql == 2 ? fy : ql == 3 ? fx0 * fx0
+                           : ql == 4 ? fx0 * fy : ql == 5 ? fy * fy : 0.f;
+            const float cb = ql == 1 ? 1.f : ql == 3 ? 2.f * fx0 : ql == 4 ? fy : 0.f;
+            const float cc2 = ql == 3 ? 1.f : 0.f;
+            const float4 *src = reinterpret_cast<const float4 *>(myWU + qd * 64 + 32 * t2 + 8 * qk);
+            const float4 d0 = src[0], d1 = src[1];
+            const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int p = 32 * t2 + 8 * qk + j;
-            int lx2, ly2;
-            tile_pixel(w * 64 + p, lx2, ly2);
-            const float fx = (float)(tx0 + lx2) - cxT, fy = (float)(ty0 + ly2) - cyT;
-#if LGM_BWD_AOP_SELECT
-            // selects, not a per-lane if-chain (whose exec-masked branches every work item's prologue paid)
-            const float dpv = myWU[min(max(ql - 6, 0), 3) * 64 + p];
-            const float f = ql == 0   ? 1.f
-                            : ql == 1 ? fx
-                            : ql == 2 ? fy
-                            : ql == 3 ? fx * fx
-                            : ql == 4 ? fx * fy
-                            : ql == 5 ? fy * fy
-                            : ql <= 9 ? dpv
-                                      : 0.f;
-#else
-            float f = 0.f;
-            if (ql == 0) f = 1.f;
-            else if (ql == 1) f = fx;
-            else if (ql == 2) f = fy;
-            else if (ql == 3) f = fx * fx;
-            else if (ql == 4) f = fx * fy;
-            else if (ql == 5) f = fy * fy;
-            else if (ql <= 9) f = myWU[(ql - 6) * 64 + p];
-#endif
-            const __bf16 h = (__bf16)f;
-            Ah[t2][j] = h;
-            Al[t2][j] = (__bf16)(f - (float)h);
+            for (int j = 0; j < 8; j++) {
+                const float geo = fmaf(fmaf(cc2, (float)j, cb), (float)j, ca);
+                const float f = ql <= 5 ? geo : ql <= 9 ? dv[j] : 0.f;
+                const __bf16 h = (__bf16)f;
+                Ah[t2][j] = h;
+                Al[t2][j] = (__bf16)(f - (float)h);
+            }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -1043,7 +1015,7 @@ int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, fl
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
                                        image, depth, alpha,
-                                       (float *)(ws + L.final_T), (int *)(ws + L.n_contrib),
+                                       (float *)(ws + L.final_T), (int *)(ws + L.n_contrib), (int *)(ws + L.wlast),
                                        (unsigned char *)(ws + L.cmask), (float4 *)(ws + L.cfin),
                                        (float *)(ws + L.ck), (int2 *)(ws + L.cklist), (int *)(ws + L.nck),
                                        (unsigned *)(ws + L.misc) + 4, L.ck_region)));
@@ -1082,7 +1054,7 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
                                        (const float *)(ws + L.final_T), (const int *)(ws + L.n_contrib),
-                                       (const float4 *)(ws + L.cfin), (const float *)(ws + L.ck),
+                                       (const int *)(ws + L.wlast), (const float4 *)(ws + L.cfin), (const float *)(ws + L.ck),
                                        (const int2 *)(ws + L.cklist), (const int *)(ws + L.nck),
                                        (const unsigned *)(ws + L.misc) + 4, L.ck_region, d_image, d_depth, d_alpha,
                                        (const unsigned char *)(ws + L.cmask), (float *)(ws + L.accum),

@@ -67,3 +67,39 @@ def test_scene_sharded_gpu(cuda, tmp_path):
         s0, s1 = z["rng"]
         np.testing.assert_array_equal(z["img"], img.numpy()[s0:s1])  # the forward is deterministic
         assert rel_l2(z["dg"], full.numpy()[s0:s1]) < 1e-5
+
+
+def _rccl_worker(tmp):
+    """One rank on cuda:0 with the nccl (= RCCL) backend: the collectives bench.py and the view-sharded backward
+    issue, on a real RCCL communicator. (RCCL takes one GPU per rank, so the test box -- one GPU -- runs a
+    single-rank group; the 2..8-rank runs are the driver's.)"""
+    import torch.distributed as dist
+    info = D.rank_info()
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=info.rank, world_size=info.world, device_id=dev)
+    try:
+        g, cv, cvp, bg, d_img, d_alpha = _case()
+        _, dg = _render(g[:1], cv[:1], cvp[:1], bg, d_img[:1], d_alpha[:1], 64)
+        grad = dg.to(dev)
+        # the view-sharded backward's in-place SUM (a one-rank group: the sum is the tensor itself); the RankInfo
+        # stand-in only opens allreduce_scene_grads' world > 1 gate, the collective runs on the real group
+        summed = D.allreduce_scene_grads(grad.clone(), D.RankInfo(0, 2, 0))
+        flat = torch.randn(3_000_001, generator=torch.Generator().manual_seed(5)).to(dev)
+        red = D.allreduce_bucketed(flat.clone(), 1_000_000, D.RankInfo(0, 2, 0), bf16=False)  # averages by 2
+        mx = D.max_over_ranks(3.5, D.RankInfo(0, 2, 0), dev)
+        torch.cuda.synchronize()
+        np.savez(os.path.join(tmp, "rccl.npz"), grad=grad.cpu().numpy(), summed=summed.cpu().numpy(),
+                 flat=flat.cpu().numpy(), red=red.cpu().numpy(), mx=np.array(mx),
+                 backend=np.array(dist.get_backend()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_collectives_single_rank(cuda, tmp_path):
+    D.spawn_ranks(_rccl_worker, 1, str(tmp_path))
+    z = np.load(os.path.join(tmp_path, "rccl.npz"))
+    assert str(z["backend"]) == "nccl"
+    np.testing.assert_array_equal(z["summed"], z["grad"])
+    np.testing.assert_allclose(z["red"], z["flat"] / 2, rtol=0, atol=0)
+    assert float(z["mx"]) == 3.5

@@ -208,7 +208,7 @@ __device__ __forceinline__ void init_sentinel(Stage &S) {
 
 // k_render_fwd: grid (B*V*T), block 256.
 #ifndef LGM_FWD_WPE
-#define LGM_FWD_WPE 6  // all B*V*T workgroups of the cfg3 launch are co-resident at 6 waves per SIMD (<= 80 VGPRs)
+#define LGM_FWD_WPE 7  // <= 72 VGPRs (spills outside the compositing loop only): 327 vs 336 us at 6, 411 at 8 (pool)
 #endif
 template <bool LOSS>  // LGM_RENDER_FUSED_LOSS compiled in (its epilogue registers stay out of the plain kernel)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE))) void k_render_fwd(Dims d, long long slot_stride, const int *__restrict__ order,

@@ -159,13 +159,13 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                 // the backward's per-view gradient accumulators start at zero (a repeated backward clears them with
                 // LGM_RENDER_BACKWARD_AGAIN); int64 fixed point in deterministic mode
                 if (d.options & LGM_RENDER_DETERMINISTIC) {
-                    ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(accum) + k * (NACC / 2);
+                    ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(accum) + k * (NACC_V / 2);
 #pragma unroll
-                    for (int q = 0; q < NACC / 2; q++) a2[q] = make_ulonglong2(0ull, 0ull);
+                    for (int q = 0; q < NACC_V / 2; q++) a2[q] = make_ulonglong2(0ull, 0ull);
                 } else {
-                    float2 *a2 = reinterpret_cast<float2 *>(accum + k * NACC);
+                    float2 *a2 = reinterpret_cast<float2 *>(accum + k * NACC_V);
 #pragma unroll
-                    for (int q = 0; q < NACC / 2; q++) a2[q] = make_float2(0.f, 0.f);
+                    for (int q = 0; q < NACC_V / 2; q++) a2[q] = make_float2(0.f, 0.f);
                 }
             } else {
                 gP[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -173,6 +173,16 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                 rects[k] = make_uint2(0u, 0u);
             }
             if (radii_out) radii_out[k] = vis ? o.radius : 0;
+            if (bv % d.V == 0) {  // the scene's view-independent record (opacity, colour), once per scene
+                const size_t ks = (size_t)d.BV * d.N * NACC_V + ((size_t)b * d.N + i) * NACC_S;
+                if (d.options & LGM_RENDER_DETERMINISTIC) {
+                    ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(reinterpret_cast<unsigned long long *>(accum) + ks);
+                    a2[0] = make_ulonglong2(0ull, 0ull);
+                    a2[1] = make_ulonglong2(0ull, 0ull);
+                } else {
+                    *reinterpret_cast<float4 *>(accum + ks) = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
         }
     }
     int nc = 0;

@@ -14,7 +14,16 @@
 namespace lgm {
 
 constexpr int BX = 16, BY = 16, TILE_PIX = BX * BY;  // 256 pixels per tile = 4 wavefronts (8x8 quadrants)
-constexpr int NACC = 10;                             // per-(view, Gaussian) screen-space gradient record
+constexpr int NACC = 10;  // gradient partials per (view, Gaussian): mean2D(2) conic(3) opacity rgb(3) depth
+// Accumulator layout (elements: fp32, or int64 fixed point in deterministic mode): the view-dependent partials
+// (mean2D, conic, depth) per (view, Gaussian) in records of NACC_V, then the view-independent ones (opacity,
+// colour) per (scene, Gaussian) in records of NACC_S -- the views of a scene add into one record, so the binning
+// zeroes and k_preproc_bwd reads 24 + 16 / V bytes per (view, Gaussian) instead of 40.
+constexpr int NACC_V = 6, NACC_S = 4;
+__host__ __device__ __forceinline__ size_t acc_index(int q, size_t bvN_i, size_t bN_i, size_t BVN) {
+    return q < 5 ? bvN_i * NACC_V + q : q < 9 ? BVN * NACC_V + bN_i * NACC_S + (q - 5) : bvN_i * NACC_V + 5;
+}
+inline size_t acc_elems(size_t B, size_t V, size_t N) { return B * V * N * NACC_V + B * N * NACC_S; }
 constexpr int LDS_HIST_MAX = 8192;                   // tiles per view for the LDS-histogram binning path
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float DET_SCALE = 4294967296.0f;  // 2^32: deterministic-mode fixed-point units per 1.0
@@ -61,7 +70,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.cklist = take((size_t)8 * L.ck_region * 8);
     L.nck = take(BV * T * 4);
     L.cmask = take(BV * P);
-    L.accum = take(BV * N * NACC * (det ? 8 : 4));
+    L.accum = take(acc_elems(B, V, N) * (det ? 8 : 4));
     L.lossp = take(BV * T * 2 * 4);  // per-tile sums of squared image / alpha residuals (fused loss)
     L.total = o;
     return L;

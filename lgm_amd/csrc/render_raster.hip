@@ -843,7 +843,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const int j = f / NACC, q = f - j * NACC;
             if (q < NV && j < CH && b0 + j < s1) {
                 const float a = sAccW[0][q * LS + j];
-                const size_t ai = (gbase + reinterpret_cast<const unsigned *>(&B.R[j])[3]) * NACC + q;
+                const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
+                const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
                 if (a != 0.f) {
                     if (DET)  // integer adds commute: order-independent sums
                         atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
@@ -891,19 +892,19 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
             if (d_means2D) { d_means2D[2 * k] = 0.f; d_means2D[2 * k + 1] = 0.f; }
             continue;
         }
-        float acc[NACC];
+        float acc[NACC_V];
         if (d.options & LGM_RENDER_DETERMINISTIC) {
-            const longlong2 *acc2 = reinterpret_cast<const longlong2 *>(accum) + k * (NACC / 2);
+            const longlong2 *acc2 = reinterpret_cast<const longlong2 *>(accum) + k * (NACC_V / 2);
 #pragma unroll
-            for (int q = 0; q < NACC / 2; q++) {
+            for (int q = 0; q < NACC_V / 2; q++) {
                 const longlong2 a = acc2[q];
                 acc[2 * q] = (float)((double)a.x * (1.0 / DET_SCALE));
                 acc[2 * q + 1] = (float)((double)a.y * (1.0 / DET_SCALE));
             }
         } else {
-            const float2 *acc2 = reinterpret_cast<const float2 *>(accum + k * NACC);
+            const float2 *acc2 = reinterpret_cast<const float2 *>(accum + k * NACC_V);
 #pragma unroll
-            for (int q = 0; q < NACC / 2; q++) {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
+            for (int q = 0; q < NACC_V / 2; q++) {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
                 const float2 a = acc2[q];
                 acc[2 * q] = a.x;
                 acc[2 * q + 1] = a.y;
@@ -911,9 +912,7 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         }
         const float dm2x = acc[0], dm2y = acc[1];
         const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
-        dop += acc[5];
-        dcol[0] += acc[6]; dcol[1] += acc[7]; dcol[2] += acc[8];
-        const float ddep = acc[9];
+        const float ddep = acc[5];
         if (d_means2D) { d_means2D[2 * k] = dm2x; d_means2D[2 * k + 1] = dm2y; }
         const float *Vw = views + 16 * bv;
         const float *Pm = projs + 16 * bv;
@@ -969,6 +968,19 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         dmean[0] += Vw[2] * ddep;
         dmean[1] += Vw[6] * ddep;
         dmean[2] += Vw[10] * ddep;
+    }
+    {  // the scene's view-independent partials (opacity, colour), summed over its views by the backward's atomics
+        const size_t ks = (size_t)d.BV * d.N * NACC_V + ((size_t)b * d.N + i) * NACC_S;
+        if (d.options & LGM_RENDER_DETERMINISTIC) {
+            const long long *a = reinterpret_cast<const long long *>(accum) + ks;
+            dop = (float)((double)a[0] * (1.0 / DET_SCALE));
+#pragma unroll
+            for (int q = 0; q < 3; q++) dcol[q] = (float)((double)a[1 + q] * (1.0 / DET_SCALE));
+        } else {
+            const float4 a = *reinterpret_cast<const float4 *>(accum + ks);
+            dop = a.x;
+            dcol[0] = a.y; dcol[1] = a.z; dcol[2] = a.w;
+        }
     }
     // ---- cov3D backward, once on the view-summed dL/dcov3D (linear, so equal to the per-view sum)
     const float dS[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
@@ -1035,7 +1047,7 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
     // the per-view accumulators were zeroed by the forward's binning; a repeated backward of the same forward
     // clears what the previous one left
     if ((d.options & LGM_RENDER_BACKWARD_AGAIN) &&
-        hipMemsetAsync(ws + L.accum, 0, (size_t)d.BV * d.N * NACC * ((d.options & LGM_RENDER_DETERMINISTIC) ? 8 : 4),
+        hipMemsetAsync(ws + L.accum, 0, acc_elems(d.B, d.V, d.N) * ((d.options & LGM_RENDER_DETERMINISTIC) ? 8 : 4),
                        st) != hipSuccess) {
         set_error("hipMemsetAsync failed");
         return LGM_E_HIP;

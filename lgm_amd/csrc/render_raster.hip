@@ -525,7 +525,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // the entry's quadrant waves at the chunk's end (then they hold the entry's gradient partials, in wave 0's slot)
     // (row NV of each wave's slot is a junk row: the MFMA results a lane does not keep are stored there, so the
     // stores need no exec-masked branches)
-    __shared__ __attribute__((aligned(16))) float sAccW[4][LS * (NV + 1)];
+    // moment rows: 0..5 geometric (w columns), then dL/dpixel-hi and dL/dpixel-lo sums of the NC colour [+ depth]
+    // channels (u columns); row NROW is the junk row
+    constexpr int NC = DEPTH ? 4 : 3, NROW = 6 + 2 * NC;
+    __shared__ __attribute__((aligned(16))) float sAccW[4][LS * (NROW + 1)];
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
     // ---- work item: (tile, chunk c, checkpoint slot)
     const int M = d.BV * d.T, Mp = LGM_XCD_ORDER ? round8(M) : M;  // head items, then the checkpoint items
@@ -629,8 +632,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #pragma unroll
     for (int rr = 0; rr < 4; rr++) {
         const int row = 4 * qk + rr;
-        const bool live = ql < MB ? row <= 5 : (row >= 6 && row < NV);
-        mrow[rr] = live ? row * LS : NV * LS;  // the junk row (all MB columns of a batch are stored)
+        const bool live = ql < MB ? row <= 5 : (row >= 6 && row < NROW);
+        mrow[rr] = live ? row * LS : NROW * LS;  // the junk row (all MB columns of a batch are stored)
     }
     float *myAcc = sAccW[w];
     float *myWU = sWU[w];
@@ -639,13 +642,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     myWU[128 + lane] = dp2;
     myWU[192 + lane] = dpd;
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // A operand: lane (ql, qk) holds feature ql at the wave pixels p = 32 t2 + 8 qk + j, j = 0..7, i.e. tile-centred
-    // fx = fx0 + j and fy = fy0 + 4 t2 + qk: the geometric features (rows 0..5) are a + b j + c j^2 with per-lane
-    // coefficients, exact in bf16 (small integers and halves); rows 6..9 are dL/dpixel, split hi + lo.
-    bf16x8 Ah[2], Al[2];
+    // A operand: lane (ql, qk) holds row ql at the wave pixels p = 32 t2 + 8 qk + j, j = 0..7, i.e. tile-centred
+    // fx = fx0 + j and fy = fy0 + 4 t2 + qk. Rows 0..5, the geometric features, are a + b j + c j^2 with per-lane
+    // coefficients, exact in bf16 (small integers and halves); rows 6..6+NC-1 are dL/dpixel rounded to bf16 and rows
+    // 6+NC.. the remainders, so A . (B_hi + B_lo) -- two MFMAs -- carries every product but lo x lo (~2^-16).
+    bf16x8 Ah[2];
     {
         const float fx0 = (float)((w & 1) << 3) - 7.5f, fy0 = (float)((w >> 1) << 3) - 7.5f;
-        const int qd = min(max(ql - 6, 0), 3);  // the dL/dpixel row of lanes 6..9
+        const bool isdp = ql >= 6 && ql < NROW, islo = ql >= 6 + NC;
+        const int qd = isdp ? (islo ? ql - 6 - NC : ql - 6) : 0;  // the dL/dpixel channel of rows 6..NROW-1
 #pragma unroll
         for (int t2 = 0; t2 < 2; t2++) {
             const float fy = fy0 + (float)(4 * t2 + qk);
@@ -659,10 +664,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 const float geo = fmaf(fmaf(cc2, (float)j, cb), (float)j, ca);
-                const float f = ql <= 5 ? geo : ql <= 9 ? dv[j] : 0.f;
-                const __bf16 h = (__bf16)f;
-                Ah[t2][j] = h;
-                Al[t2][j] = (__bf16)(f - (float)h);
+                const __bf16 dh = (__bf16)dv[j];
+                const float dlo = dv[j] - (float)dh;
+                Ah[t2][j] = ql <= 5 ? (__bf16)geo : !isdp ? (__bf16)0.f : islo ? (__bf16)dlo : dh;
             }
         }
     }
@@ -687,7 +691,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, cacc, 0, 0, 0);
-            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al[t2], bh, cacc, 0, 0, 0);
             a2[t2] = cacc;
         }
         const f32x4 acc = a2[0] + a2[1];
@@ -716,9 +719,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
         if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
         {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
-            static_assert((4 * LS * (NV + 1)) % 4 == 0, "slot zeroing by float4");
+            static_assert((4 * LS * (NROW + 1)) % 4 == 0, "slot zeroing by float4");
             float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
-            for (int q = tid; q < 4 * LS * (NV + 1) / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q = tid; q < 4 * LS * (NROW + 1) / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         int cnt;
         {
@@ -741,9 +744,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #else
         if (stager) stage_commit(S, B, tid, k < s1, id_cur, tx0, ty0, true);
         {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
-            static_assert((4 * LS * (NV + 1)) % 4 == 0, "slot zeroing by float4");
+            static_assert((4 * LS * (NROW + 1)) % 4 == 0, "slot zeroing by float4");
             float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
-            for (int q = tid; q < 4 * LS * (NV + 1) / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q = tid; q < 4 * LS * (NROW + 1) / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         __syncthreads();
         if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
@@ -813,10 +816,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const float xg = Pj.x - cxT, yg = Pj.y - cyT;
             float q[NACC];
 #pragma unroll
-            for (int qq = 0; qq < NV; qq++) {
+            for (int qq = 0; qq < NV; qq++) {  // (colour [depth] rows: the hi and the lo dL/dpixel sums)
                 float s = 0.f;
 #pragma unroll
-                for (int ww = 0; ww < 4; ww++) s += sAccW[ww][qq * LS + j];
+                for (int ww = 0; ww < 4; ww++)
+                    s += qq < 6 ? sAccW[ww][qq * LS + j] : sAccW[ww][qq * LS + j] + sAccW[ww][(qq + NC) * LS + j];
                 q[qq] = s;
             }
             const float Sx = fmaf(xg, q[0], -q[1]), Sy = fmaf(yg, q[0], -q[2]);

@@ -443,6 +443,13 @@ def run(args):
     for _ in range(args.warmup):
         step3()
     el3 = D.timed_steps(step3, args.steps, info, torch.cuda.synchronize, dev)
+    prof3 = _native.KernelProfiler()  # per-kernel times of the single-scene step (a separate, untimed pass)
+    with prof3:
+        for _ in range(args.steps):
+            step3()
+        torch.cuda.synchronize()
+    kern3 = prof3.summary()
+    prof3.close()
     if world > 1:  # the all-reduce on its own, same tensor size
         buf = torch.zeros(1, N_GAUSS, 14, device=dev)
         for _ in range(3):
@@ -454,7 +461,8 @@ def run(args):
                     f"over {world} rank(s) + SUM all-reduce of dL/dgaussians [1,N,14] fp32 (RCCL)",
         "ms_per_step": round(1e3 * el3 / args.steps, 4),
         "Mpixels_per_s": round(VIEWS * P * args.steps / el3 / 1e6, 2),
-        "allreduce_ms": round(ar["ms"], 4) if world > 1 else None}
+        "allreduce_ms": round(ar["ms"], 4) if world > 1 else None,
+        "kernels": {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in kern3.items()}}
 
     if not args.no_cfg5:  # every rank (its all-reduce is collective)
         result["cfg5"] = cfg5_bench(dev, info, max(3, args.steps // 10))

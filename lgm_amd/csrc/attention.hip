@@ -432,8 +432,20 @@ __device__ __forceinline__ typename Ty<DT>::V8 tr_frag(const typename Ty<DT>::T 
     return __builtin_bit_cast(V8, r);
 }
 
+// Waves per SIMD the compiler is held to (register cap 512 / n) for D <= 64; D = 128 stays at the compiler's
+// choice. Measured r02 (profiles/r02/ab_attn_wpe), cfg4 L=9600 C=512: forward 0.41 -> 0.34 ms at 3 (4 spills the
+// D=64 two-sub-tile forward), dQ 0.51 -> 0.45 and dK/dV 0.64 -> 0.50 ms at 2 (4 puts dK/dV in scratch: 1.43 ms).
+#ifndef LGM_ATTN_FWD_WPE
+#define LGM_ATTN_FWD_WPE 3
+#endif
+#ifndef LGM_ATTN_BWD_WPE
+#define LGM_ATTN_BWD_WPE 2
+#endif
+#ifndef LGM_ATTN_QS_MIN_GRID
+#define LGM_ATTN_QS_MIN_GRID 512  // two query sub-tiles per wave once the grid has this many workgroups
+#endif
 template <int DT, int D, int QS>
-__global__ __launch_bounds__(NT) void k_attn_fwd2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LGM_ATTN_FWD_WPE : 1))) void k_attn_fwd2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
                                                   const typename Ty<DT>::T *__restrict__ k,
                                                   const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                   typename Ty<DT>::T *__restrict__ o, float *__restrict__ lse) {
@@ -606,7 +618,7 @@ struct TileLoader {  // one 64-row tile of up to two [tokens][ld] tensors, CH 16
 
 // dK, dV: grid (ceil(L / (64 KS)), B*H); wavefront w owns keys k0 + 16 s + (lane & 15), s < KS.
 template <int DT, int D, int KS>
-__global__ __launch_bounds__(NT) void k_attn_dkdv2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LGM_ATTN_BWD_WPE : 1))) void k_attn_dkdv2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
                                                    const typename Ty<DT>::T *__restrict__ k,
                                                    const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                    const typename Ty<DT>::T *__restrict__ dout,
@@ -730,7 +742,7 @@ __global__ __launch_bounds__(NT) void k_attn_dkdv2(int L, int H, float scale, co
 
 // dQ: grid (ceil(L / (64 QS)), B*H); wavefront w owns query rows q0 + 16 s + (lane & 15), s < QS.
 template <int DT, int D, int QS>
-__global__ __launch_bounds__(NT) void k_attn_dq2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LGM_ATTN_BWD_WPE : 1))) void k_attn_dq2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
                                                  const typename Ty<DT>::T *__restrict__ k,
                                                  const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                  const typename Ty<DT>::T *__restrict__ dout,
@@ -838,7 +850,7 @@ int fwd_impl(int B, int L, int H, float scale, const void *q, const void *k, con
     if constexpr (DT != LGM_ATTN_F32) {
         // two query sub-tiles per wavefront when the grid stays large enough to fill the chip
         constexpr int QS2 = D <= 64 ? 2 : 1;
-        if (QS2 == 2 && (long long)((L + 127) / 128) * B * H >= 512) {
+        if (QS2 == 2 && (long long)((L + 127) / 128) * B * H >= LGM_ATTN_QS_MIN_GRID) {
             dim3 grid((L + 127) / 128, B * H);
             LGM_LAUNCH("k_attn_fwd", st, (k_attn_fwd2<DT, D, QS2><<<grid, NT, 0, st>>>(
                                               L, H, scale, (const T *)q, (const T *)k, (const T *)v, ld, (T *)o, lse)));

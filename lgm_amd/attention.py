@@ -139,6 +139,75 @@ class MemEffAttention(Attention):
         return self._attend(x)
 
 
+def _autocast_dtype(dev_type: str):
+    if torch.is_autocast_enabled(dev_type):
+        return torch.get_autocast_dtype(dev_type)
+    return None
+
+
+class _NormTokens(torch.autograd.Function):
+    """GroupNorm of x [B*F, C, H, W] straight into MVAttention's token layout [B, F*H*W, C] (core/unet.py:40-42) in
+    one HIP pass (lgm_mva_norm_tokens). Backward: torch's GroupNorm backward on the un-permuted gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, F: int, groups: int, eps: float, tok_dtype):
+        BF, C, H, W = x.shape
+        B, HW = BF // F, H * W
+        x = x.contiguous()
+        tok = torch.empty((B, F * HW, C), device=x.device, dtype=tok_dtype)
+        mean = torch.empty((BF, groups), device=x.device, dtype=torch.float32)
+        rstd = torch.empty((BF, groups), device=x.device, dtype=torch.float32)
+        w = None if weight is None else weight.detach().float().contiguous()
+        b = None if bias is None else bias.detach().float().contiguous()
+        nat.check(nat.lib().lgm_mva_norm_tokens(_dtype_code(x), _dtype_code(tok), B, F, C, HW, groups, float(eps),
+                                                nat.ptr(x), nat.ptr(w), nat.ptr(b), nat.ptr(tok), nat.ptr(mean),
+                                                nat.ptr(rstd), nat.stream_of(x.device)), "lgm_mva_norm_tokens")
+        ctx.save_for_backward(x, weight, mean, rstd)
+        ctx.shape = (B, F, C, H, W, groups)
+        return tok
+
+    @staticmethod
+    def backward(ctx, d_tok):
+        x, weight, mean, rstd = ctx.saved_tensors
+        B, F, C, H, W, groups = ctx.shape
+        g = d_tok.reshape(B, F, H, W, C).permute(0, 1, 4, 2, 3).reshape(B * F, C, H, W).float().contiguous()
+        mask = [ctx.needs_input_grad[0], weight is not None and ctx.needs_input_grad[1],
+                weight is not None and ctx.needs_input_grad[2]]
+        dx, dw, db = torch.ops.aten.native_group_norm_backward(g, x.float(), mean, rstd,
+                                                               None if weight is None else weight.float(), B * F, C,
+                                                               H * W, groups, mask)
+        dx = None if dx is None else dx.to(x.dtype)
+        dw = None if dw is None else dw.to(weight.dtype)
+        db = None if db is None else db.to(weight.dtype)
+        return dx, dw, db, None, None, None, None
+
+
+class _TokensOut(torch.autograd.Function):
+    """MVAttention's [B, F*H*W, C] -> [B*F, C, H, W] permute fused with (y + res) * skip_scale (core/unet.py:45-48),
+    one HIP pass (lgm_mva_tokens_out); res None: the permute alone."""
+
+    @staticmethod
+    def forward(ctx, y, res, F: int, H: int, W: int, skip: float):
+        B, L, C = y.shape
+        y = y.contiguous()
+        out_dtype = y.dtype if res is None else torch.promote_types(y.dtype, res.dtype)
+        out = torch.empty((B * F, C, H, W), device=y.device, dtype=out_dtype)
+        r = None if res is None else res.contiguous()
+        nat.check(nat.lib().lgm_mva_tokens_out(_dtype_code(y), 0 if r is None else _dtype_code(r), _dtype_code(out),
+                                               B, F, C, H * W, nat.ptr(y), nat.ptr(r), float(skip), nat.ptr(out),
+                                               nat.stream_of(y.device)), "lgm_mva_tokens_out")
+        ctx.meta = (B, F, C, H, W, float(skip), y.dtype, None if res is None else res.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        B, F, C, H, W, skip, ydt, rdt = ctx.meta
+        g = d_out if rdt is None else d_out * skip
+        d_y = g.reshape(B, F, C, H, W).permute(0, 1, 3, 4, 2).reshape(B, F * H * W, C).to(ydt)
+        d_res = None if rdt is None else g.to(rdt)
+        return d_y, d_res, None, None, None, None
+
+
 class MVAttention(nn.Module):
     """core/unet.py:11-49: self-attention across the tokens of all `num_frames` views of an object.
 
@@ -154,12 +223,22 @@ class MVAttention(nn.Module):
         self.num_frames = num_frames
         self.norm = nn.GroupNorm(num_groups=groups, num_channels=dim, eps=eps, affine=True)
         self.attn = MemEffAttention(dim, num_heads, qkv_bias, proj_bias, attn_drop, proj_drop)
+        self.fused = True  # GPU: the HIP GroupNorm->tokens and tokens->residual kernels (False: torch ops, as upstream)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         BV, C, H, W = x.shape
         if BV % self.num_frames:
             raise ValueError(f"batch {BV} is not a multiple of num_frames={self.num_frames}")
         B = BV // self.num_frames
+        if self.fused and x.is_cuda and x.dtype in _DTYPES and C // self.norm.num_groups <= 256:
+            # fused token layout kernels around the attention core (same math; GroupNorm in fp32 as under autocast)
+            ac = _autocast_dtype("cuda")
+            tok_dtype = ac if ac is not None else x.dtype
+            tok = _NormTokens.apply(x, self.norm.weight, self.norm.bias, self.num_frames, self.norm.num_groups,
+                                    self.norm.eps, tok_dtype)
+            y = self.attn(tok)
+            return _TokensOut.apply(y, x if self.residual else None, self.num_frames, H, W,
+                                    self.skip_scale if self.residual else 1.0)
         res = x
         x = self.norm(x)
         x = x.reshape(B, self.num_frames, C, H, W).permute(0, 1, 3, 4, 2).reshape(B, -1, C)

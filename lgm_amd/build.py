@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/common.hip", "csrc/render_bin.hip", "csrc/render_raster.hip", "csrc/render_api.hip",
-           "csrc/attention.hip", "csrc/head.hip"]
+           "csrc/attention.hip", "csrc/head.hip", "csrc/mvattn.hip"]
 OUT = os.path.join(HERE, "_lib", "liblgm_amd.so")
 ARCH = os.environ.get("LGM_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -124,6 +124,48 @@ def test_module_bf16_autocast(cuda, path):
     assert rel_l2(x.grad.float().cpu().numpy(), z["dx"]) < 5e-2
 
 
+MVA_CASES = [  # C, heads, frames, H, W, batch -- LGM levels (D = 32 / 64) and ragged ones (Cg = 3: scalar stores)
+    (512, 16, 6, 16, 16, 1), (1024, 16, 6, 10, 10, 1), (256, 8, 4, 8, 8, 2), (96, 3, 2, 7, 5, 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["f32", "bf16_autocast"])
+@pytest.mark.parametrize("case", MVA_CASES, ids=lambda c: "x".join(map(str, c)))
+def test_mvattention_fused_layout_matches_torch_ops(cuda, case, mode):
+    """MVAttention's fused GroupNorm->tokens and tokens->residual kernels (lgm_mva_*) against the same module on
+    upstream's torch ops (fused=False): forward, dL/dx and the GroupNorm / Linear parameter gradients. fp32: the
+    only difference is the order of the GroupNorm sums (1e-5); bf16: tokens may round to neighbouring bf16 values
+    (1e-2)."""
+    from lgm_amd.attention import MVAttention
+    C, heads, frames, H, W, B = case
+    torch.manual_seed(11)
+    m = MVAttention(C, heads, num_frames=frames, skip_scale=0.5 ** 0.5).to(cuda)
+    with torch.no_grad():
+        m.norm.weight.uniform_(0.5, 1.5)
+        m.norm.bias.uniform_(-0.2, 0.2)
+    x0 = torch.randn(B * frames, C, H, W, device=cuda) * 2 + 0.3
+    gy = torch.randn(B * frames, C, H, W, device=cuda)
+    outs = []
+    for fused in (True, False):
+        m.fused = fused
+        m.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        if mode == "f32":
+            y = m(x)
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = m(x)
+        y.float().backward(gy)
+        outs.append((y.dtype, y.detach().float(), x.grad.float(), {k: p.grad.float() for k, p in m.named_parameters()}))
+    tol = 1e-5 if mode == "f32" else 1e-2
+    (tf, yf, dxf, gf), (tt, yt, dxt, gt) = outs
+    assert tf == tt
+    assert rel_l2(yf.cpu().numpy(), yt.cpu().numpy()) < tol
+    assert rel_l2(dxf.cpu().numpy(), dxt.cpu().numpy()) < 10 * tol
+    for k in gt:
+        assert rel_l2(gf[k].cpu().numpy(), gt[k].cpu().numpy()) < 10 * tol, k
+
+
 SHAPES = [  # B, L, H, D -- LGM levels (4 views x 8^2 / 16^2 / 32^2 tokens, D = 64 / 64 / 32) and ragged edges
     (1, 256, 16, 64), (2, 1024, 16, 64), (1, 4096, 16, 32), (1, 1, 2, 32), (3, 65, 2, 64), (2, 100, 3, 128),
     (1, 17, 1, 32), (2, 600, 4, 32), (2, 4100, 16, 32),  # the last one: two query sub-tiles per wave + a tail

@@ -48,12 +48,15 @@ int lgm_attn_backward(int dtype, int B, int L, int H, int D, float scale, const 
  * biased variance) of x [B*F, C, HW] (NCHW, dtype_x) written in the token layout of core/unet.py:41-42,
  * tokens[b][f*HW + hw][c] (dtype_tok: what the qkv Linear consumes, bf16 under autocast). gamma/beta fp32 [C]
  * (NULL: 1/0). mean/rstd [B*F, groups] fp32 are saved for the backward (torch's native_group_norm_backward).
+ * workspace: lgm_mva_workspace_size bytes of device scratch (per-chunk statistics; deterministic merge).
  * Replaces the GroupNorm module call + reshape/permute/reshape copy + autocast cast of the reference.
  *
  * lgm_mva_tokens_out: out[b*F+f][c][hw] = (y[b][f*HW + hw][c] + res[b*F+f][c][hw]) * skip (core/unet.py:45-48:
  * reshape/permute back, residual, skip_scale); res NULL: out = the permuted y. out is contiguous [B*F, C, HW]. */
+size_t lgm_mva_workspace_size(int B, int F, int C, int HW, int groups); /* chunk statistics, bytes */
 int lgm_mva_norm_tokens(int dtype_x, int dtype_tok, int B, int F, int C, int HW, int groups, float eps, const void *x,
-                        const float *gamma, const float *beta, void *tokens, float *mean, float *rstd, void *stream);
+                        const float *gamma, const float *beta, void *tokens, float *mean, float *rstd, void *workspace,
+                        size_t workspace_bytes, void *stream);
 int lgm_mva_tokens_out(int dtype_y, int dtype_res, int dtype_out, int B, int F, int C, int HW, const void *y,
                        const void *res, float skip, void *out, void *stream);
 

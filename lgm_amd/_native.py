@@ -32,8 +32,9 @@ SIGNATURES = {
     "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _c_ll, _vp, _c_size, _vp]),
     "lgm_attn_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "lgm_mva_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "lgm_mva_norm_tokens": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp,
-                                     _vp, _vp, _vp, _vp]),
+                                     _vp, _vp, _vp, _vp, _c_size, _vp]),
     "lgm_mva_tokens_out": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _vp,
                                     _vp]),
     "lgm_render_forward_loss": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float,

@@ -159,9 +159,12 @@ class _NormTokens(torch.autograd.Function):
         rstd = torch.empty((BF, groups), device=x.device, dtype=torch.float32)
         w = None if weight is None else weight.detach().float().contiguous()
         b = None if bias is None else bias.detach().float().contiguous()
-        nat.check(nat.lib().lgm_mva_norm_tokens(_dtype_code(x), _dtype_code(tok), B, F, C, HW, groups, float(eps),
-                                                nat.ptr(x), nat.ptr(w), nat.ptr(b), nat.ptr(tok), nat.ptr(mean),
-                                                nat.ptr(rstd), nat.stream_of(x.device)), "lgm_mva_norm_tokens")
+        L_ = nat.lib()
+        ws_bytes = L_.lgm_mva_workspace_size(B, F, C, HW, groups)
+        ws = torch.empty(max(ws_bytes, 1), device=x.device, dtype=torch.uint8)
+        nat.check(L_.lgm_mva_norm_tokens(_dtype_code(x), _dtype_code(tok), B, F, C, HW, groups, float(eps), nat.ptr(x),
+                                         nat.ptr(w), nat.ptr(b), nat.ptr(tok), nat.ptr(mean), nat.ptr(rstd),
+                                         nat.ptr(ws), ws_bytes, nat.stream_of(x.device)), "lgm_mva_norm_tokens")
         ctx.save_for_backward(x, weight, mean, rstd)
         ctx.shape = (B, F, C, H, W, groups)
         return tok
@@ -230,7 +233,7 @@ class MVAttention(nn.Module):
         if BV % self.num_frames:
             raise ValueError(f"batch {BV} is not a multiple of num_frames={self.num_frames}")
         B = BV // self.num_frames
-        if self.fused and x.is_cuda and x.dtype in _DTYPES and C // self.norm.num_groups <= 256:
+        if self.fused and x.is_cuda and x.dtype in _DTYPES:
             # fused token layout kernels around the attention core (same math; GroupNorm in fp32 as under autocast)
             ac = _autocast_dtype("cuda")
             tok_dtype = ac if ac is not None else x.dtype

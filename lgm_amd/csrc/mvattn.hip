@@ -1,11 +1,11 @@
 // lgm_amd/csrc/mvattn.hip -- the token layout changes around MVAttention's attention core (core/unet.py:35-49),
 // fused with the GroupNorm before and the residual after:
-//   k_mva_norm   GroupNorm(x) of [B*F, C, H, W] (core/unet.py:40, fp32 statistics), written straight into the
-//                [B, F*H*W, C] token layout of :41-42 in the qkv Linear's input dtype (bf16 under autocast): one
-//                kernel instead of torch's moments / fused-params / normalise launches + the permute copy + the cast.
+//   k_mva_stats + k_mva_norm   GroupNorm(x) of [B*F, C, H, W] (core/unet.py:40, fp32 statistics), written
+//                straight into the [B, F*H*W, C] token layout of :41-42 in the qkv Linear's input dtype (bf16 under
+//                autocast): two launches instead of torch's moments / fused-params / normalise launches + the
+//                permute copy + the cast.
 //   k_mva_out    the [B, F*H*W, C] -> [B*F, C, H, W] permute of :45-46 fused with (x + res) * skip_scale of :47-48.
-// Both are HBM-bound layout kernels: 64x64 LDS-tiled transposes (k_mva_out) or per-thread channel runs stored as
-// 16-B vectors (k_mva_norm), so every global access is a full 64-B+ segment.
+// Both are HBM-bound layout kernels: 64x64 LDS-tiled transposes, so global reads and writes run along rows.
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 
@@ -33,57 +33,98 @@ __device__ __forceinline__ float block_sum256(float v, float *red) {
     return (red[0] + red[1]) + (red[2] + red[3]);  // fixed order: every thread gets the same value
 }
 
-// grid (G, B*F), block 256: one (sample, group). Two passes over the group for mean and (centred) variance -- the
-// group's Cg*HW elements are contiguous and stay in L2 -- then y = x * (rstd gamma) + (beta - mean rstd gamma)
-// (torch's fused GroupNorm parameters) written to token rows: thread hw stores its Cg channels as 16-B vectors.
+// GroupNorm statistics in two launches, all deterministic:
+// k_mva_stats  grid (S, G, B*F): chunk s of group g of sample bf (the group's Cg*HW elements are contiguous) ->
+//              its mean and centred sum of squares (two passes over the chunk, which stays in L1/L2).
+// k_mva_norm   grid (ceil(HW/64), ceil(C/64), B*F): merges the chunk statistics of the groups its 64 channels
+//              belong to (Chan's parallel formula, fixed order), then normalises a 64-channel x 64-pixel tile
+//              through LDS: reads along hw, writes token rows along c. y = x (rstd gamma) + (beta - mean rstd gamma),
+//              torch's fused GroupNorm parameters.
+constexpr int MVA_CHUNK = 4096;  // elements per statistics workgroup
+
+__device__ __forceinline__ int mva_chunks(int n) { return (n + MVA_CHUNK - 1) / MVA_CHUNK; }
+
+template <class TI>
+__global__ __launch_bounds__(256) void k_mva_stats(int C, int HW, int G, const TI *__restrict__ x,
+                                                   float2 *__restrict__ part) {
+    __shared__ float red[4];
+    const int s = blockIdx.x, g = blockIdx.y, bf = blockIdx.z, Cg = C / G, tid = threadIdx.x;
+    const int n = Cg * HW, S = mva_chunks(n);
+    const int i0 = s * MVA_CHUNK, i1 = min(n, i0 + MVA_CHUNK), m = i1 - i0;
+    const TI *xg = x + ((size_t)bf * C + (size_t)g * Cg) * HW;
+    float v[MVA_CHUNK / 256];
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < MVA_CHUNK / 256; k++) {
+        const int i = i0 + k * 256 + tid;
+        const float t = to_f(xg[i < i1 ? i : i0]);  // unconditional loads (clamped index): all in flight at once
+        v[k] = i < i1 ? t : 0.f;
+        sum += v[k];
+    }
+    const float mean = block_sum256(sum, red) / (float)m;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < MVA_CHUNK / 256; k++) {
+        const float d = i0 + k * 256 + tid < i1 ? v[k] - mean : 0.f;
+        q = fmaf(d, d, q);
+    }
+    q = block_sum256(q, red);
+    if (tid == 0) part[((size_t)bf * G + g) * S + s] = make_float2(mean, q);
+}
+
 template <class TI, class TO>
 __global__ __launch_bounds__(256) void k_mva_norm(int F, int C, int HW, int G, float eps, const TI *__restrict__ x,
                                                   const float *__restrict__ gamma, const float *__restrict__ beta,
-                                                  TO *__restrict__ tok, float *__restrict__ mean_out,
-                                                  float *__restrict__ rstd_out) {
-    __shared__ float red[4];
-    __shared__ float sa[256], sb[256];  // per-channel scale / shift (Cg <= 256)
-    const int g = blockIdx.x, bf = blockIdx.y, Cg = C / G, tid = threadIdx.x;
-    const int n = Cg * HW;
-    const TI *xg = x + ((size_t)bf * C + (size_t)g * Cg) * HW;
-    float s = 0.f;
-    for (int i = tid; i < n; i += 256) s += to_f(xg[i]);
-    const float mean = block_sum256(s, red) / (float)n;
-    float v = 0.f;
-    for (int i = tid; i < n; i += 256) {
-        const float d = to_f(xg[i]) - mean;
-        v = fmaf(d, d, v);
+                                                  const float2 *__restrict__ part, TO *__restrict__ tok,
+                                                  float *__restrict__ mean_out, float *__restrict__ rstd_out) {
+    __shared__ float tile[64][65];  // [pixel][channel]
+    __shared__ float sa[64], sb[64];
+    const int hw0 = blockIdx.x * 64, c0 = blockIdx.y * 64, bf = blockIdx.z, tid = threadIdx.x;
+    const int Cg = C / G, n = Cg * HW, S = mva_chunks(n);
+    if (tid < 64 && c0 + tid < C) {  // this channel's group statistics (Chan merge of the chunks, in order)
+        const int c = c0 + tid, g = c / Cg;
+        const float2 *pg = part + ((size_t)bf * G + g) * S;
+        float mean = 0.f, M2 = 0.f;
+        int cnt = 0;
+        for (int s2 = 0; s2 < S; s2++) {
+            const float2 p = pg[s2];
+            const int m = min(n, (s2 + 1) * MVA_CHUNK) - s2 * MVA_CHUNK;
+            const int tot = cnt + m;
+            const float d = p.x - mean;
+            mean = fmaf(d, (float)m / (float)tot, mean);
+            M2 += p.y + d * d * ((float)cnt * (float)m / (float)tot);
+            cnt = tot;
+        }
+        const float rstd = rsqrtf(fmaxf(M2 / (float)n, 0.f) + eps);  // biased variance, as torch
+        const float a = rstd * (gamma ? gamma[c] : 1.f);
+        sa[tid] = a;
+        sb[tid] = (beta ? beta[c] : 0.f) - mean * a;
+        if (blockIdx.x == 0 && c % Cg == 0) {  // one writer per (sample, group)
+            mean_out[(size_t)bf * G + g] = mean;
+            rstd_out[(size_t)bf * G + g] = rstd;
+        }
     }
-    const float var = block_sum256(v, red) / (float)n;  // biased, as torch
-    const float rstd = rsqrtf(fmaxf(var, 0.f) + eps);
-    for (int c = tid; c < Cg; c += 256) {
-        const float a = rstd * (gamma ? gamma[g * Cg + c] : 1.f);
-        sa[c] = a;
-        sb[c] = (beta ? beta[g * Cg + c] : 0.f) - mean * a;
+    __syncthreads();
+    const TI *xb = x + (size_t)bf * C * HW;
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {  // all 16 loads issued before the first use (clamped, unconditional addresses)
+        const int i = tid + 256 * k, r = i >> 6, h = i & 63;  // channel r, pixel h
+        const bool ok = hw0 + h < HW && c0 + r < C;
+        v[k] = to_f(xb[ok ? (size_t)(c0 + r) * HW + hw0 + h : 0]);
     }
-    if (tid == 0) {
-        mean_out[(size_t)bf * G + g] = mean;
-        rstd_out[(size_t)bf * G + g] = rstd;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int i = tid + 256 * k, r = i >> 6, h = i & 63;
+        tile[h][r] = fmaf(v[k], sa[r], sb[r]);
     }
     __syncthreads();
     const int b = bf / F, f = bf - b * F;
-    constexpr int VEC = 16 / sizeof(TO);  // channels per 16-B store
-    const bool vec = (Cg % VEC) == 0 && (C % VEC) == 0;
-    for (int hw = tid; hw < HW; hw += 256) {
-        TO *row = tok + ((size_t)b * F * HW + (size_t)f * HW + hw) * C + (size_t)g * Cg;
-        if (vec) {
-            for (int c0 = 0; c0 < Cg; c0 += VEC) {
-                union { uint4 u; TO e[VEC]; } pk;
+    TO *tb = tok + ((size_t)b * F * HW + (size_t)f * HW) * C;
 #pragma unroll
-                for (int k = 0; k < VEC; k++) {
-                    const int c = c0 + k;
-                    pk.e[k] = from_f<TO>(fmaf(to_f(xg[(size_t)c * HW + hw]), sa[c], sb[c]));
-                }
-                *reinterpret_cast<uint4 *>(row + c0) = pk.u;
-            }
-        } else {
-            for (int c = 0; c < Cg; c++) row[c] = from_f<TO>(fmaf(to_f(xg[(size_t)c * HW + hw]), sa[c], sb[c]));
-        }
+    for (int k = 0; k < 16; k++) {
+        const int i = tid + 256 * k, r = i >> 6, c = i & 63;  // token row r, channel c
+        if (hw0 + r < HW && c0 + c < C) tb[(size_t)(hw0 + r) * C + c0 + c] = from_f<TO>(tile[r][c]);
     }
 }
 
@@ -97,31 +138,53 @@ __global__ __launch_bounds__(256) void k_mva_out(int F, int C, int HW, const TY 
     const int hw0 = blockIdx.x * 64, c0 = blockIdx.y * 64, bf = blockIdx.z, tid = threadIdx.x;
     const int b = bf / F, f = bf - b * F;
     const TY *yb = y + ((size_t)b * F * HW + (size_t)f * HW) * C;
-    for (int i = tid; i < 64 * 64; i += 256) {
-        const int r = i >> 6, c = i & 63;  // token row r, channel c
-        if (hw0 + r < HW && c0 + c < C) tile[c][r] = to_f(yb[(size_t)(hw0 + r) * C + c0 + c]);
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {  // all loads in flight before the first use (clamped, unconditional addresses)
+        const int i = tid + 256 * k, r = i >> 6, c = i & 63;  // token row r, channel c
+        const bool ok = hw0 + r < HW && c0 + c < C;
+        v[k] = to_f(yb[ok ? (size_t)(hw0 + r) * C + c0 + c : 0]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int i = tid + 256 * k, r = i >> 6, c = i & 63;
+        tile[c][r] = v[k];
+    }
+    float rv[16];
+    if (res) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int i = tid + 256 * k, r = i >> 6, h = i & 63;  // channel r, pixel h
+            const bool ok = hw0 + h < HW && c0 + r < C;
+            rv[k] = to_f(res[ok ? ((size_t)bf * C + c0 + r) * HW + hw0 + h : 0]);
+        }
     }
     __syncthreads();
-    for (int i = tid; i < 64 * 64; i += 256) {
-        const int r = i >> 6, h = i & 63;  // channel r, pixel h
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int i = tid + 256 * k, r = i >> 6, h = i & 63;  // channel r, pixel h
         if (hw0 + h < HW && c0 + r < C) {
             const size_t o = ((size_t)bf * C + c0 + r) * HW + hw0 + h;
-            float v = tile[r][h];
+            float t = tile[r][h];
             if (res) {
-                v += to_f(res[o]);
-                v = to_f(from_f<TO>(v));  // (exact for an fp32 output)
-                v *= skip;
+                t += rv[k];
+                t = to_f(from_f<TO>(t));  // (exact for an fp32 output)
+                t *= skip;
             }
-            out[o] = from_f<TO>(v);
+            out[o] = from_f<TO>(t);
         }
     }
 }
 
 template <class TI, class TO>
 int launch_norm(int B, int F, int C, int HW, int G, float eps, const void *x, const float *gamma, const float *beta,
-                void *tok, float *mean, float *rstd, hipStream_t st) {
-    LGM_LAUNCH("k_mva_norm", st, (k_mva_norm<TI, TO><<<dim3(G, B * F), 256, 0, st>>>(
-                                      F, C, HW, G, eps, (const TI *)x, gamma, beta, (TO *)tok, mean, rstd)));
+                void *tok, float *mean, float *rstd, float2 *part, hipStream_t st) {
+    const int S = (C / G * HW + MVA_CHUNK - 1) / MVA_CHUNK;
+    LGM_LAUNCH("k_mva_stats", st,
+               (k_mva_stats<TI><<<dim3(S, G, B * F), 256, 0, st>>>(C, HW, G, (const TI *)x, part)));
+    const dim3 grid((HW + 63) / 64, (C + 63) / 64, B * F);
+    LGM_LAUNCH("k_mva_norm", st, (k_mva_norm<TI, TO><<<grid, 256, 0, st>>>(F, C, HW, G, eps, (const TI *)x, gamma,
+                                                                            beta, part, (TO *)tok, mean, rstd)));
     return LGM_OK;
 }
 
@@ -135,11 +198,11 @@ int launch_out(int B, int F, int C, int HW, const void *y, const void *res, floa
 
 template <class TI>
 int norm_by_out(int dto, int B, int F, int C, int HW, int G, float eps, const void *x, const float *gamma,
-                const float *beta, void *tok, float *mean, float *rstd, hipStream_t st) {
+                const float *beta, void *tok, float *mean, float *rstd, float2 *part, hipStream_t st) {
     switch (dto) {
-        case LGM_ATTN_F32: return launch_norm<TI, float>(B, F, C, HW, G, eps, x, gamma, beta, tok, mean, rstd, st);
-        case LGM_ATTN_BF16: return launch_norm<TI, __hip_bfloat16>(B, F, C, HW, G, eps, x, gamma, beta, tok, mean, rstd, st);
-        case LGM_ATTN_F16: return launch_norm<TI, __half>(B, F, C, HW, G, eps, x, gamma, beta, tok, mean, rstd, st);
+        case LGM_ATTN_F32: return launch_norm<TI, float>(B, F, C, HW, G, eps, x, gamma, beta, tok, mean, rstd, part, st);
+        case LGM_ATTN_BF16: return launch_norm<TI, __hip_bfloat16>(B, F, C, HW, G, eps, x, gamma, beta, tok, mean, rstd, part, st);
+        case LGM_ATTN_F16: return launch_norm<TI, __half>(B, F, C, HW, G, eps, x, gamma, beta, tok, mean, rstd, part, st);
     }
     set_error("lgm_mva_norm_tokens: bad output dtype %d", dto);
     return LGM_E_INVALID;
@@ -172,28 +235,39 @@ int out_by_r(int dtr, int dto, int B, int F, int C, int HW, const void *y, const
 }  // namespace
 }  // namespace lgm
 
+extern "C" size_t lgm_mva_workspace_size(int B, int F, int C, int HW, int groups) {
+    if (B <= 0 || F <= 0 || C <= 0 || HW <= 0 || groups <= 0 || C % groups) return 0;
+    const size_t S = ((size_t)(C / groups) * HW + lgm::MVA_CHUNK - 1) / lgm::MVA_CHUNK;
+    return (size_t)B * F * groups * S * sizeof(float2);
+}
+
 extern "C" int lgm_mva_norm_tokens(int dtype_x, int dtype_tok, int B, int F, int C, int HW, int groups, float eps,
                                    const void *x, const float *gamma, const float *beta, void *tokens, float *mean,
-                                   float *rstd, void *stream) {
+                                   float *rstd, void *workspace, size_t workspace_bytes, void *stream) {
     lgm::clear_error();
-    if (B < 0 || F <= 0 || C <= 0 || HW < 0 || groups <= 0 || C % groups || C / groups > 256) {
+    if (B < 0 || F <= 0 || C <= 0 || HW < 0 || groups <= 0 || C % groups) {
         lgm::set_error("lgm_mva_norm_tokens: bad shape B=%d F=%d C=%d HW=%d groups=%d", B, F, C, HW, groups);
         return LGM_E_INVALID;
     }
     if (B == 0 || HW == 0) return LGM_OK;
-    if (!x || !tokens || !mean || !rstd) {
+    if (!x || !tokens || !mean || !rstd || !workspace) {
         lgm::set_error("lgm_mva_norm_tokens: null pointer");
         return LGM_E_INVALID;
     }
+    if (workspace_bytes < lgm_mva_workspace_size(B, F, C, HW, groups)) {
+        lgm::set_error("lgm_mva_norm_tokens: workspace too small");
+        return LGM_E_WORKSPACE;
+    }
+    float2 *part = (float2 *)workspace;
     hipStream_t st = (hipStream_t)stream;
     switch (dtype_x) {
         case LGM_ATTN_F32:
-            return lgm::norm_by_out<float>(dtype_tok, B, F, C, HW, groups, eps, x, gamma, beta, tokens, mean, rstd, st);
+            return lgm::norm_by_out<float>(dtype_tok, B, F, C, HW, groups, eps, x, gamma, beta, tokens, mean, rstd, part, st);
         case LGM_ATTN_BF16:
             return lgm::norm_by_out<__hip_bfloat16>(dtype_tok, B, F, C, HW, groups, eps, x, gamma, beta, tokens, mean,
-                                                    rstd, st);
+                                                    rstd, part, st);
         case LGM_ATTN_F16:
-            return lgm::norm_by_out<__half>(dtype_tok, B, F, C, HW, groups, eps, x, gamma, beta, tokens, mean, rstd, st);
+            return lgm::norm_by_out<__half>(dtype_tok, B, F, C, HW, groups, eps, x, gamma, beta, tokens, mean, rstd, part, st);
     }
     lgm::set_error("lgm_mva_norm_tokens: bad input dtype %d", dtype_x);
     return LGM_E_INVALID;

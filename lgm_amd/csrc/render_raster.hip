@@ -87,6 +87,9 @@ struct StageT {                                   // PAD: list padding = entries
 #endif
 using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 // the backward sits 3 workgroups per CU only just: its LDS must stay <= 53,744 B (measured: 53,776 B ran at 2)
+#ifndef LGM_BWD_EARLY_STAGE
+#define LGM_BWD_EARLY_STAGE 1  // the first chunk's staging goes out before the per-pixel state loads (bwd 647 -> 644 us)
+#endif
 #ifndef LGM_BWD_CHUNK
 #define LGM_BWD_CHUNK 64  // backward entries per staged chunk (the per-wave moment slots scale with it)
 #endif
@@ -558,6 +561,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     int n;
     tile_range(tile, slot_stride, tile_start, tile_count, base, n);
     const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base);
+#if LGM_BWD_EARLY_STAGE
+    // the first chunk's ids and LDS DMA go out before the per-pixel state loads (bounded by the list length n, a
+    // superset of [s0, s1): rows past s1 are staged but never listed or flushed), so their two dependent memory
+    // round trips overlap the pixel loads instead of following them
+    const bool stager = tid < BWD_CHUNK;
+    const int s0e = c * TILE_PIX;
+    unsigned id_cur = stager && s0e + tid < n ? ids[s0e + tid] : 0u;
+    if (stager && s0e + tid < n) stage_dma(S.buf[0], w, id_cur, (size_t)bv * d.N, b, d.N, gP, gQ, gauss);
+    unsigned id_next = stager && s0e + BWD_CHUNK + tid < n ? ids[s0e + BWD_CHUNK + tid] : 0u;
+#endif
     const size_t P = (size_t)d.H * d.W;
     const size_t pid = inside ? (size_t)d.W * py + px : 0;
     const float T_final = inside ? final_T[bv * P + pid] : 0.f;
@@ -614,8 +627,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const int wlast = w == 0 ? wl4.x : w == 1 ? wl4.y : w == 2 ? wl4.z : wl4.w;
     const int nlist = min(n, max(max(wl4.x, wl4.y), max(wl4.z, wl4.w)));
     const int s0 = c * TILE_PIX;
+#if LGM_BWD_EARLY_STAGE
+    if (s0 >= nlist) {  // workgroup-uniform
+        vm_wait_all();
+        return;
+    }
+#else
     if (s0 >= nlist) return;  // workgroup-uniform
+#endif
     const int s1 = (c + 1 <= nck[tile]) ? min(nlist, s0 + TILE_PIX) : nlist;
+#if LGM_BWD_EARLY_STAGE
+    if (s0 >= s1) {  // (nothing to do; the early DMA must land before the workgroup retires)
+        vm_wait_all();
+        return;
+    }
+#endif
     const unsigned long long t_item = d.counters ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const float bg_dot = bg[0] * dp0 + bg[1] * dp1 + bg[2] * dp2;
     float cdpf = fmaf(cf.x, dp0, fmaf(cf.y, dp1, cf.z * dp2));
@@ -704,10 +730,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // Staging pipeline (front to back over [s0, s1)): chunk b0 + CH streams into the other buffer by LDS DMA
     // during chunk b0's compositing and is complete (vm_wait_all) before chunk b0's gradient atomics are issued,
     // so no staging load queues behind them; the sorted ids run one chunk further ahead in a register.
+#if !LGM_BWD_EARLY_STAGE
     const bool stager = tid < CH;  // the threads that stage (and test) one chunk row each
     unsigned id_cur = stager && s0 + tid < s1 ? ids[s0 + tid] : 0u;
     if (stager && s0 + tid < s1) stage_dma(S.buf[0], w, id_cur, gbase, b, d.N, gP, gQ, gauss);
     unsigned id_next = stager && s0 + CH + tid < s1 ? ids[s0 + CH + tid] : 0u;
+#endif
     vm_wait_all();
     int cur = 0;
     for (int b0 = s0; b0 < s1; b0 += CH, cur ^= 1) {

@@ -20,6 +20,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "lgm_attn.h"
 
@@ -435,6 +437,14 @@ __device__ __forceinline__ typename Ty<DT>::V8 tr_frag(const typename Ty<DT>::T 
 // Waves per SIMD the compiler is held to (register cap 512 / n) for D <= 64; D = 128 stays at the compiler's
 // choice. Measured r02 (profiles/r02/ab_attn_wpe), cfg4 L=9600 C=512: forward 0.41 -> 0.34 ms at 3 (4 spills the
 // D=64 two-sub-tile forward), dQ 0.51 -> 0.45 and dK/dV 0.64 -> 0.50 ms at 2 (4 puts dK/dV in scratch: 1.43 ms).
+// LDS row stride of the 16-bit K/V/Q/dO tiles: D + 16 elements (row stride 24 / 40 / 72 dwords for D = 32 / 64 /
+// 128, i.e. 24, 40 or 8 mod 64) puts the 16 lanes of every ds_read_b128 group on 16 distinct 4-bank slots and the 8
+// rows of each ds_read_b64_tr_b16 half on disjoint 8-bank ranges: conflict-free. D + 8 (20 / 36 / 68 dwords) was
+// 2-way on both (SQ_LDS_BANK_CONFLICT = half of the forward's LDS cycles, profiles/r02/pmc_attn). Measured
+// (profiles/r02/ab_attn_pad): D = 64 fwd / dQ / dK,dV -5 / -8 / -10 %; D = 32 unchanged.
+#ifndef LGM_ATTN_LDK_PAD
+#define LGM_ATTN_LDK_PAD 16
+#endif
 #ifndef LGM_ATTN_FWD_WPE
 #define LGM_ATTN_FWD_WPE 3
 #endif
@@ -451,7 +461,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
                                                   typename Ty<DT>::T *__restrict__ o, float *__restrict__ lse) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr int LDK = D + 8;                         // 16-B padded rows: conflict-free b128 row reads
+    constexpr int LDK = D + LGM_ATTN_LDK_PAD;          // padded rows (see LGM_ATTN_LDK_PAD)
     constexpr int CH = 64 * D * 2 / 16 / NT;           // 16-B chunks per thread per tile (K or V)
     static_assert(CH >= 1, "tile too small for the loader");
     __shared__ __attribute__((aligned(16))) T Ks[2][64 * LDK];
@@ -503,7 +513,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
     store_regs(0);
     __syncthreads();
     int cur = 0;
-    for (int kb = 0; kb < L; kb += 64) {
+    // one 64-key tile; TAIL: the last, partial tile (keys >= L masked): full tiles run a body without the masking
+    // code. (An unconditional rescale instead of the branch below measured the same: profiles/r02/ab_attn_pad.)
+    auto step = [&](int kb, auto tail) {
+        constexpr bool TAIL = decltype(tail)::value;
         const bool more = kb + 64 < L;
         if (more) load_regs(kb + 64);  // in flight during this tile's compute
         const T *Kt = Ks[cur], *Vt = Vs[cur];
@@ -523,7 +536,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
                 sacc[s][sub] = a;
             }
         }
-        if (kb + 64 > L) {  // tail tile: keys >= L
+        if (TAIL) {  // tail tile: keys >= L
 #pragma unroll
             for (int sub = 0; sub < 4; sub++)
 #pragma unroll
@@ -572,7 +585,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
         if (more) store_regs(cur ^ 1);  // buffer cur^1 was last read before the previous barrier
         __syncthreads();
         cur ^= 1;
-    }
+    };
+    const int kfull = L & ~63;
+    for (int kb = 0; kb < kfull; kb += 64) step(kb, std::false_type{});
+    if (kfull < L) step(kfull, std::true_type{});
 #pragma unroll
     for (int s = 0; s < QS; s++) {
         const int qr = q0 + 16 * s + r16;
@@ -627,7 +643,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
                                                    typename Ty<DT>::T *__restrict__ dv, long long ldd) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr int LDK = D + 8;
+    constexpr int LDK = D + LGM_ATTN_LDK_PAD;
     __shared__ __attribute__((aligned(16))) T Qs[2][64 * LDK];
     __shared__ __attribute__((aligned(16))) T Os[2][64 * LDK];
     __shared__ float sl[2][64], sd[2][64];
@@ -750,7 +766,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
                                                  typename Ty<DT>::T *__restrict__ dq, long long ldd) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr int LDK = D + 8;
+    constexpr int LDK = D + LGM_ATTN_LDK_PAD;
     __shared__ __attribute__((aligned(16))) T Ks[2][64 * LDK];
     __shared__ __attribute__((aligned(16))) T Vs[2][64 * LDK];
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;

@@ -10,6 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/common.hip", "csrc/render_bin.hip", "csrc/render_raster.hip", "csrc/render_api.hip",
            "csrc/attention.hip", "csrc/head.hip", "csrc/mvattn.hip"]
+# per-source extra flags. attention.hip: no NaN semantics -- its max / exp chains then skip the quieting
+# canonicalisations clang inserts before every fmaxf of an MFMA result (the render kernels keep IEEE NaN handling:
+# degenerate-Gaussian tests such as !(det > 0) rely on it)
+FILE_FLAGS = {"csrc/attention.hip": ["-fno-honor-nans"]}
 OUT = os.path.join(HERE, "_lib", "liblgm_amd.so")
 ARCH = os.environ.get("LGM_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -38,9 +42,10 @@ def build(force: bool = False, verbose: bool = False, out: str = None, defines=(
     tag = "" if out == OUT else "." + os.path.basename(out)
     for src in sources():
         obj = os.path.join(HERE, "_lib", os.path.basename(src) + tag + ".o")
+        extra = FILE_FLAGS.get(os.path.relpath(src, HERE), [])
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
                "-munsafe-fp-atomics", "-fno-slp-vectorize", "-I", os.path.join(ROOT, "include"), "-I",
-               os.path.join(HERE, "csrc"), "-c", src, "-o", obj] + \
+               os.path.join(HERE, "csrc"), "-c", src, "-o", obj] + extra + \
             [d if d.startswith("-") else f"-D{d}" for d in defines]  # A/B variants: defines or extra flags
         if verbose:
             print(" ".join(cmd))

@@ -647,6 +647,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     float cdpf = fmaf(cf.x, dp0, fmaf(cf.y, dp1, cf.z * dp2));
     if (DEPTH) cdpf = fmaf(cf.w, dpd, cdpf);
     const float DK = cdpf - (dpa - bg_dot) * T_final;  // Dfin - K
+    float Erem = DK - Dup;  // Dfin - K - D_i, kept directly (one subtraction less per entry)
     const float ddelx_dx = 0.5f * d.W, ddely_dy = 0.5f * d.H;
     const size_t gbase = (size_t)bv * d.N;
     // MFMA operands: A (features) lane (ql, qk) holds feature ql of wave pixels 32 t + 8 qk + j, j = 0..7
@@ -783,6 +784,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         const int cnt = compact_wave(S, w, lane, 0, wlast - b0);  // positions < wlast only
 #endif
         static_assert(MB == 8, "one batch = two 4-entry list words");
+        const int lastrel = last - b0;  // this pixel's last contributor, relative to the chunk
         uint2 lraw[2];  // the next step's list words, read one step ahead
         list_raw<MB>(S, w, 0, lraw);
         for (int kk = 0; kk < cnt; kk += MB) {
@@ -805,13 +807,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    const int pos = b0 + jj8[4 * h + u];  // 0-based position in the tile list
+                    const bool before_last = jj8[4 * h + u] < lastrel;  // position b0 + jj < last
                     const float4 Pj = Pv[u], Q = Qv[u];
                     cc[u].w = Q.w;
                     const float dx = Pj.x - pfx, dy = Pj.y - pfy;
                     const float lp = fmaf(Q.x * dy, dy, fmaf(fmaf(Pj.w, dy, Pj.z * dx), dx, Q.y));  // as k_render_fwd
                     const float e = __builtin_amdgcn_exp2f(lp);  // opacity G
-                    const bool ok = pos < last && lp <= Q.y && e >= 1.0f / 255.0f;
+                    const bool ok = before_last && lp <= Q.y && e >= 1.0f / 255.0f;
                     al[u] = ok ? alpha_cap(e) : 0.f;
                     Gw[u] = ok ? e : 0.f;  // dL/dG = opacity dL/dalpha (0: the entry adds nothing here)
                 }
@@ -822,9 +824,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                     float cdp = fmaf(cu.x, dp0, fmaf(cu.y, dp1, cu.z * dp2));
                     if (DEPTH) cdp = fmaf(cu.w, dpd, cdp);
                     const float aT = alpha * Tr;
-                    Dup = fmaf(aT, cdp, Dup);
                     const float inv = __builtin_amdgcn_rcpf(1.f - alpha);  // 1 / (1 - alpha), 1 ulp
-                    const float dL_dalpha = fmaf(Tr, cdp, -(DK - Dup) * inv);
+                    Erem = fmaf(-aT, cdp, Erem);
+                    const float dL_dalpha = fmaf(Tr, cdp, -Erem * inv);
                     Tr = Tr - aT;
                     myWU[(4 * h + u) * WU_LD + lane] = Gw[u] * dL_dalpha;  // w
                     myWU[(MB + 4 * h + u) * WU_LD + lane] = aT;            // u (dchannel_dcolor)

@@ -282,3 +282,38 @@ def test_deterministic_backward(cuda, oracle_mod):
     out = {"image": img.detach().cpu().numpy(), "alpha": alp.detach().cpu().numpy(),
            "d_gaussians": grads[0].cpu().numpy()}
     _check(oracle_mod, out, g, cv, cvp, 256, 256, bg, d_m, d_alpha)
+
+
+# ------------------------------------------------------------------------------------------- headline workload
+def test_headline_pool_batched_equals_per_scene(cuda, oracle_mod):
+    """bench.py's headline workload itself: the 8-scene scaling pool (seed 2, 100k Gaussians x 6 views
+    x 256^2 per scene, upstream gradients seed 1002) rendered as ONE batched call, as at N = 1, equals the same
+    scenes rendered one per call, as each rank renders its shard at N = 8: forward bit for bit, and in
+    deterministic mode (order-independent fixed-point accumulation) the gradients bit for bit too. Scene 0 of the
+    pool is checked against the oracle on the production path (clamp, image + alpha backward)."""
+    from lgm_amd.gs import rasterize
+    B, N, V, R = 8, 100_000, 6, 256
+    pool = synthetic_gaussians(B, N, seed=2)
+    cv, cvp, _ = orbit_cameras(V)
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(B, V, R, R, seed=1002)
+
+    def run(g, c, cp, di, da):
+        gd = g.to(cuda).requires_grad_(True)
+        img, _, alp = rasterize(gd, c.to(cuda), cp.to(cuda), bg.to(cuda), TAN, TAN, R, R, clamp=True,
+                                deterministic=True)
+        torch.autograd.backward([img, alp], [di.to(cuda), da.to(cuda)])
+        return img.detach(), alp.detach(), gd.grad
+
+    cvb = cv[None].expand(B, -1, -1, -1).contiguous()
+    cvpb = cvp[None].expand(B, -1, -1, -1).contiguous()
+    img_b, alp_b, grad_b = run(pool, cvb, cvpb, d_img, d_alpha)
+    for s in range(B):
+        img_s, alp_s, grad_s = run(pool[s:s + 1], cv[None], cvp[None], d_img[s:s + 1], d_alpha[s:s + 1])
+        assert torch.equal(img_b[s:s + 1], img_s), f"scene {s}: image differs batched vs alone"
+        assert torch.equal(alp_b[s:s + 1], alp_s), f"scene {s}: alpha differs batched vs alone"
+        assert torch.equal(grad_b[s:s + 1], grad_s), f"scene {s}: gradient differs batched vs alone"
+    # scene 0 on the production (non-deterministic, float-atomic) path vs the oracle
+    g0, c0, cp0 = pool[0:1], cv[None], cvp[None]
+    d_m, keep = _clamp_masked_grads(oracle_mod, g0, c0, cp0, R, R, bg, d_img[0:1])
+    out = _production(cuda, g0, c0, cp0, R, R, bg, d_img[0:1], d_alpha[0:1], keep)
+    _check(oracle_mod, out, g0, c0, cp0, R, R, bg, d_m, d_alpha[0:1])

@@ -39,8 +39,9 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// k_bin: grid (ceil(N / BIN_G), B*V), block BIN_THREADS, one Gaussian per thread. A workgroup's LDS tile
-// histogram aggregates its BIN_G Gaussians before one global reservation per touched tile.
+// k_bin: grid (ceil(N / BIN_G), B * ceil(V / BIN_ITERS)), block BIN_THREADS, one Gaussian per thread; the workgroup
+// bins its BIN_G Gaussians into BIN_ITERS views of one scene, one view (batch) after the other. A workgroup's LDS
+// tile histogram aggregates its BIN_G Gaussians before one global reservation per touched tile of the view.
 //
 // Load balance: a Gaussian's work is the tile rows of its candidate rectangle (1 to tens). Each wavefront
 // flattens the rows of its 64 Gaussians into one list and takes 64 at a time (lane -> (Gaussian, row); the owner
@@ -55,6 +56,12 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 #endif
 #ifndef LGM_BIN_ITERS
 #define LGM_BIN_ITERS 3  // measured: 1 -> 50 us, 2 -> 55, 3 -> 46, 4 -> 58 (cfg3)
+#endif
+#ifndef LGM_BIN_VIEWLOOP
+// 1: a workgroup's BIN_ITERS batches are BIN_ITERS VIEWS of the same BIN_G Gaussians (each Gaussian row loaded once
+// per workgroup instead of once per view: pool 199 -> 193 us, single scene 40.6 -> 38.8 us); 0: BIN_ITERS
+// consecutive Gaussian batches of one view (then the next batch's rows are prefetched, LGM_BIN_PREFETCH)
+#define LGM_BIN_VIEWLOOP 1
 #endif
 constexpr int BIN_THREADS = LGM_BIN_THREADS, BIN_G = BIN_THREADS, BIN_ITERS = LGM_BIN_ITERS;
 constexpr int BIN_HITCAP = BIN_THREADS * 6;  // hit-list capacity (typical: ~4 hits per Gaussian)
@@ -102,7 +109,14 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     __shared__ unsigned short sRank[BIN_HITCAP];  // rank of the hit within its tile (this workgroup)
     __shared__ int s_nhit;
     __shared__ unsigned long long s_tot[2];
-    const int bv = blockIdx.y, b = bv / d.V, T = d.T, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int T = d.T, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+#if LGM_BIN_VIEWLOOP
+    const int vgroups = (d.V + BIN_ITERS - 1) / BIN_ITERS;
+    const int b = blockIdx.y / vgroups, vg0 = (blockIdx.y - b * vgroups) * BIN_ITERS;
+    int bv = b * d.V + vg0;  // the batch's view (updated per batch; `dest` reads it by reference)
+#else
+    const int bv = blockIdx.y, b = bv / d.V;
+#endif
     const bool lds = T <= LDS_HIST_MAX;
     int *hbase = hist + T, *fill = hist + 2 * T;
     int *cur = tile_count + (size_t)bv * T;
@@ -131,24 +145,31 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     // the previous batch (registers), so only the first batch waits for its loads.
     float gnext[14];
     {
-        const int i0 = (blockIdx.x * BIN_ITERS) * BIN_G + tid;
+        const int i0 = (LGM_BIN_VIEWLOOP ? blockIdx.x : blockIdx.x * BIN_ITERS) * BIN_G + tid;
         if (i0 < d.N) load_gaussian(gauss + ((size_t)b * d.N + i0) * 14, gnext);
     }
     for (int it = 0; it < BIN_ITERS; it++) {
+#if LGM_BIN_VIEWLOOP
+    if (vg0 + it >= d.V) break;  // workgroup-uniform (the last view group of a scene may be short)
+    bv = b * d.V + vg0 + it;
+    cur = tile_count + (size_t)bv * T;
+    const int i = blockIdx.x * BIN_G + tid;
+#else
+    const int i = (blockIdx.x * BIN_ITERS + it) * BIN_G + tid;
+#endif
     if (tid == 0) s_nhit = 0;
     if (lds)
         for (int t = tid; t < T; t += BIN_THREADS) hist[t] = 0;
     // ---- preprocess, one Gaussian per thread
-    const int i = (blockIdx.x * BIN_ITERS + it) * BIN_G + tid;
     Geo o;
     bool vis = false;
     float g[14];
 #pragma unroll
     for (int q = 0; q < 14; q++) g[q] = gnext[q];
-    if (LGM_BIN_PREFETCH && it + 1 < BIN_ITERS && i + BIN_G < d.N)
+    if (!LGM_BIN_VIEWLOOP && LGM_BIN_PREFETCH && it + 1 < BIN_ITERS && i + BIN_G < d.N)
         load_gaussian(gauss + ((size_t)b * d.N + i + BIN_G) * 14, gnext);  // the next batch's row, in flight
     if (i < d.N) {
-        if (!LGM_BIN_PREFETCH && it > 0) load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
+        if (!LGM_BIN_VIEWLOOP && !LGM_BIN_PREFETCH && it > 0) load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
         vis = preprocess_one(g, views + 16 * bv, projs + 16 * bv, d, o);
         if (MODE != COUNT) {
             const size_t k = (size_t)bv * d.N + i;
@@ -910,7 +931,11 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     unsigned long long *pairs = (unsigned long long *)(ws + L.pairs), *misc = (unsigned long long *)(ws + L.misc);
     float *accum = (float *)(ws + L.accum);
     const size_t lds = d.T <= LDS_HIST_MAX ? 3 * (size_t)d.T * 4 : 0;
+#if LGM_BIN_VIEWLOOP
+    dim3 grid((d.N + BIN_G - 1) / BIN_G, d.B * ((d.V + BIN_ITERS - 1) / BIN_ITERS));
+#else
     dim3 grid((d.N + BIN_G * BIN_ITERS - 1) / (BIN_G * BIN_ITERS), d.BV);
+#endif
     if (d.N > 0) {
         if (count_only || !L.slot) {
             LGM_LAUNCH("k_bin_count", st, (k_bin<COUNT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,

@@ -235,8 +235,11 @@ def test_integer_parity_tile_lists(cuda, oracle_mod, name):
 
 def test_exact_count_path_matches_slot_path_512(cuda, monkeypatch):
     """The packed workspace (exact pair count first, one host sync; taken when the slot workspace exceeds the
-    budget) gives the slot path's forward bit for bit and its gradient up to float-atomic ordering, at cfg4's
-    512^2 (1,024 tiles per view) with 6 of the 20 views."""
+    budget) gives the slot path's results bit for bit, at cfg4's 512^2 (1,024 tiles per view) with 5 of the 20
+    views: the forward always, the gradients in deterministic mode (order-independent fixed-point accumulation, so
+    only the tile-list addressing differs between the two runs). (A float-atomic comparison of the two is a draw
+    of the accumulation order: ill-conditioned rotation gradients of needle-like Gaussians then differ by up to
+    ~1e-3 relative between ANY two runs, slot or packed.)"""
     from lgm_amd import gs as lgs
     g = synthetic_gaussians(1, 153_600, seed=4)
     cv, cvp, _ = orbit_cameras(20)
@@ -244,20 +247,19 @@ def test_exact_count_path_matches_slot_path_512(cuda, monkeypatch):
     V = cv.shape[1]
     d_img, _, d_alpha, bg = synthetic_upstream_grads(1, V, 512, 512, seed=45)
     keep = torch.ones(1)
+    monkeypatch.setenv("LGM_AMD_DETERMINISTIC", "1")
     outs = []
-    for budget in (None, None, 0):
+    for budget in (None, 0):
         monkeypatch.setattr(lgs, "_WS_BUDGET", budget)
         outs.append(_production(cuda, g, cv, cvp, 512, 512, bg, d_img, d_alpha, keep))
-    slot, slot2, packed = outs
-    for k in ("image", "alpha"):
+    slot, packed = outs
+    for k in ("image", "alpha", "d_gaussians"):
         assert np.array_equal(slot[k], packed[k]), k
-    # the same sums in a different float-atomic order: within the gradient bar (1e-4), or within 3x the
-    # run-to-run spread of the slot path itself where float-atomic ordering alone exceeds it (ill-conditioned
-    # rotation gradients of needle-like Gaussians)
-    for name, sl in GROUPS.items():
-        noise = rel_l2(slot2["d_gaussians"][..., sl], slot["d_gaussians"][..., sl])
-        e = rel_l2(packed["d_gaussians"][..., sl], slot["d_gaussians"][..., sl])
-        assert e < max(BWD_TOL, 3.0 * noise), f"d_{name}: {e:.3e} (slot rerun spread {noise:.3e})"
+    monkeypatch.setenv("LGM_AMD_DETERMINISTIC", "0")
+    monkeypatch.setattr(lgs, "_WS_BUDGET", 0)  # the packed path with float atomics: same forward, bit for bit
+    fl = _production(cuda, g, cv, cvp, 512, 512, bg, d_img, d_alpha, keep)
+    for k in ("image", "alpha"):
+        assert np.array_equal(slot[k], fl[k]), k
 
 
 def test_deterministic_backward(cuda, oracle_mod):

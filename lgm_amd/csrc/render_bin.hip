@@ -140,9 +140,10 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
             t_ph = t;
         }
     };
-    // BIN_ITERS batches of BIN_G Gaussians per workgroup, one after the other: fewer, longer workgroups fit the
-    // launch into one round of residency (3 workgroups per CU by LDS). Each batch's Gaussian rows are loaded during
-    // the previous batch (registers), so only the first batch waits for its loads.
+    // BIN_ITERS batches per workgroup, one after the other: fewer, longer workgroups (2 per CU: 106 VGPRs at 8 waves
+    // per workgroup) fit the single scene's launch into one round of residency. View loop: the batches are views
+    // of the same Gaussians, whose rows are loaded once; otherwise each batch's rows are loaded during the previous
+    // batch (registers), so only the first batch waits for its loads.
     float gnext[14];
     {
         const int i0 = (LGM_BIN_VIEWLOOP ? blockIdx.x : blockIdx.x * BIN_ITERS) * BIN_G + tid;

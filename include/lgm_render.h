@@ -110,7 +110,7 @@ int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *worksp
  * iterations of one wavefront; then 8 entries per tile t (B*V*T tiles): s_memrealtime stamps (100 MHz)
  * [8+8t] fwd start, [+1] fwd end, [+2], [+3] unused (the backward keeps per-work-item records), [+4] sort start,
  * [+5] sort end, and [+6] the tile's binned list length; then 8 entries per binning workgroup
- * (B*V*ceil(N/512)): phase stamps [0] start, [1] preprocessed, [2] tile tests done, [3] reserved, [4] end,
+ * (room for B*V*ceil(N/512); the binning launch uses its first B*ceil(V/3)*ceil(N/512)): phase stamps [0] start, [1] preprocessed, [2] tile tests done, [3] reserved, [4] end,
  * and [5] its binned pairs; then 4 entries per backward work item: start/end stamps, (entries | chunk << 20 |
  * tile << 40) and one unused -- so the buffer must hold 8 + 8*B*V*tiles + 8*B*V*ceil(N/512) +
  * 4*5*B*V*tiles entries.

@@ -17,7 +17,7 @@ g = synthetic_gaussians(B, 100000, seed=1 if B == 1 else 2).to(dev).requires_gra
 cv, cvp, cp = (t[None].expand(B, *t.shape).contiguous().to(dev) for t in orbit_cameras(6))
 d_img, _, d_alpha, bg = synthetic_upstream_grads(B, 6, 256, 256, seed=1001 if B == 1 else 1002)
 M = B * 6 * 256
-NB = B * 6 * ((100000 + 511) // 512)  # binning records reserved (k_bin uses the first B*6*ceil(N / 1536))
+NB = B * 6 * ((100000 + 511) // 512)  # binning records reserved (k_bin uses the first B*ceil(6/3)*ceil(N/512): 3 views per workgroup)
 NI = 5 * M  # backward work-item capacity
 cnt = torch.zeros(8 + 8 * M + 8 * NB + 4 * NI, dtype=torch.int64, device=dev)
 L = _native.lib()

@@ -14,7 +14,8 @@
  *   lse     : [B, H, L] fp32, natural-log row log-sum-exp of scale * q k^T (saved for the backward).
  *   d_o     : [B, L, H, D] contiguous; dq/dk/dv: same layout as q/k/v with row stride ld_dqkv.
  * D must be 32, 64 or 128 (LGM's UNet: 16 heads over 512 or 1024 channels -> D = 32 or 64); accumulation is fp32.
- * All work is enqueued on `stream` (a hipStream_t, NULL = default stream); nothing synchronises.
+ * All work is enqueued on `stream` (a hipStream_t, NULL = default stream); nothing synchronises. `diag`: per-call
+ * diagnostics (lgm_common.h), NULL = none.
  */
 #ifndef LGM_ATTN_H
 #define LGM_ATTN_H
@@ -35,12 +36,13 @@ size_t lgm_attn_workspace_size(int dtype, int B, int L, int H);
 
 /* o = softmax(scale * q k^T) v per (batch, head); also writes lse. */
 int lgm_attn_forward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,
-                     const void *v, long long ld_qkv, void *o, float *lse, void *stream);
+                     const void *v, long long ld_qkv, void *o, float *lse, void *stream, const lgm_diag *diag);
 
 /* dq, dk, dv of the forward above given d_o (o and lse from the forward). Overwrites dq/dk/dv. */
 int lgm_attn_backward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,
                       const void *v, long long ld_qkv, const void *o, const float *lse, const void *d_o, void *dq,
-                      void *dk, void *dv, long long ld_dqkv, void *workspace, size_t workspace_bytes, void *stream);
+                      void *dk, void *dv, long long ld_dqkv, void *workspace, size_t workspace_bytes, void *stream,
+                      const lgm_diag *diag);
 
 /* MVAttention's token layout around the core (core/unet.py:35-49), fused with its GroupNorm and residual.
  *
@@ -56,9 +58,9 @@ int lgm_attn_backward(int dtype, int B, int L, int H, int D, float scale, const 
 size_t lgm_mva_workspace_size(int B, int F, int C, int HW, int groups); /* chunk statistics, bytes */
 int lgm_mva_norm_tokens(int dtype_x, int dtype_tok, int B, int F, int C, int HW, int groups, float eps, const void *x,
                         const float *gamma, const float *beta, void *tokens, float *mean, float *rstd, void *workspace,
-                        size_t workspace_bytes, void *stream);
+                        size_t workspace_bytes, void *stream, const lgm_diag *diag);
 int lgm_mva_tokens_out(int dtype_y, int dtype_res, int dtype_out, int B, int F, int C, int HW, const void *y,
-                       const void *res, float skip, void *out, void *stream);
+                       const void *res, float skip, void *out, void *stream, const lgm_diag *diag);
 
 #ifdef __cplusplus
 }

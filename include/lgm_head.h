@@ -13,7 +13,8 @@
  * Conventions: DEVICE pointers, contiguous. dtype 0 = fp32, 1 = bf16 for x / dx (the UNet runs under bf16
  * autocast in training, core/options.py:89-104 mixed_precision='bf16'); weight [14,14] (the conv's [14,14,1,1]),
  * bias [14] (may be NULL: zero), gaussians / d_gaussians [B, V*h*w, 14] and d_weight / d_bias are fp32.
- * Returns 0 or a negative LGM_E* code (lgm_last_error()); stream-ordered, no host synchronisation.
+ * Returns 0 or a negative LGM_E* code (lgm_last_error()); stream-ordered, no host synchronisation; `diag`: per-call
+ * diagnostics (lgm_common.h), NULL = none.
  */
 #ifndef LGM_HEAD_H
 #define LGM_HEAD_H
@@ -33,14 +34,14 @@ size_t lgm_gaussian_head_workspace_size(int B, int V, int h, int w);
  * the [B, N, 4] slice (core/models.py:43,112); the backward needs them. */
 int lgm_gaussian_head_forward(int dtype, int B, int V, int h, int w, const void *x, const float *weight,
                               const float *bias, float *gaussians, float *rot_norm, void *workspace,
-                              size_t workspace_bytes, void *stream);
+                              size_t workspace_bytes, void *stream, const lgm_diag *diag);
 
 /* d_gaussians -> dx (x's dtype and layout, overwritten), d_weight [14,14] and d_bias [14] (overwritten; d_bias
  * may be NULL). rot_norm: the forward's. */
 int lgm_gaussian_head_backward(int dtype, int B, int V, int h, int w, const void *x, const float *weight,
                                const float *bias, const float *rot_norm, const float *d_gaussians, void *dx,
                                float *d_weight, float *d_bias, void *workspace, size_t workspace_bytes,
-                               void *stream);
+                               void *stream, const lgm_diag *diag);
 
 #ifdef __cplusplus
 }

@@ -21,7 +21,8 @@
  * Error behaviour: every entry point returns 0 on success and a negative LGM_E* code on failure; it never
  * throws across the ABI. lgm_last_error() returns a thread-local description of the last failure.
  * Threading: stream-ordered (all work is enqueued on `stream`, a hipStream_t passed as void*), no host
- * synchronisation inside forward/backward, reentrant; no global mutable state other than the error string.
+ * synchronisation inside forward/backward, reentrant; no global mutable state other than the error string: every
+ * behaviour switch is a per-call `options` bit and diagnostics are a per-call `diag` (lgm_common.h; NULL = none).
  * Memory: caller-owned. Scratch and saved-for-backward state live in ONE caller-allocated workspace whose size
  * is given by lgm_render_workspace_size(); the same workspace must be passed, untouched, to the backward.
  */
@@ -49,7 +50,8 @@ size_t lgm_render_workspace_size(int B, int V, int N, int H, int W, long long pa
  * call lgm_render_forward with that pair_capacity. */
 int lgm_render_count_pairs(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
                            const float *cam_view_proj, float tanfovx, float tanfovy, float scale_modifier,
-                           void *workspace, size_t workspace_bytes, long long *pairs_out, void *stream);
+                           void *workspace, size_t workspace_bytes, long long *pairs_out, void *stream,
+                           const lgm_diag *diag);
 
 /* Forward of all B x V renders (replaces B*V calls of _C.rasterize_gaussians). radii_out [B,V,N] int32 may be
  * NULL. stats_out, if not NULL, is a DEVICE int64[2] with the counts described at lgm_render_count_pairs. */
@@ -57,7 +59,7 @@ int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians
                        const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                        float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
                        void *workspace, size_t workspace_bytes, long long pair_capacity, long long *stats_out,
-                       int options, void *stream);
+                       int options, void *stream, const lgm_diag *diag);
 
 /* Backward of all B x V renders (replaces B*V calls of _C.rasterize_gaussians_backward plus the autograd sum
  * over views). d_image / d_depth / d_alpha may be NULL (treated as zero). Writes d_gaussians [B,N,14] (overwrites).
@@ -66,7 +68,7 @@ int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussian
                         const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
                         float *d_gaussians, float *d_means2D, void *workspace, size_t workspace_bytes,
-                        long long pair_capacity, int options, void *stream);
+                        long long pair_capacity, int options, void *stream, const lgm_diag *diag);
 
 /* Loss-fused variants for training (core/models.py:133-167): with gt_images [B,V,3,H,W] and gt_masks [B,V,1,H,W]
  * (DEVICE fp32), the forward also composites the ground truth over bg (gt * mask + bg * (1 - mask)) and writes
@@ -81,13 +83,13 @@ int lgm_render_forward_loss(int B, int V, int N, int H, int W, const float *gaus
                             const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                             float scale_modifier, float *image, float *depth, float *alpha, const float *gt_images,
                             const float *gt_masks, float *loss_out, void *workspace, size_t workspace_bytes,
-                            long long pair_capacity, int options, void *stream);
+                            long long pair_capacity, int options, void *stream, const lgm_diag *diag);
 int lgm_render_backward_loss(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
                              const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                              float scale_modifier, const float *d_image, const float *d_alpha,
                              const float *gt_images, const float *gt_masks, const float *d_loss,
                              float *d_gaussians, void *workspace, size_t workspace_bytes, long long pair_capacity,
-                             int options, void *stream);
+                             int options, void *stream, const lgm_diag *diag);
 
 /* Inspection of the state a forward left in its workspace (the equivalent of upstream's saved binningBuffer /
  * imgBuffer: point_list + ranges, n_contrib, accum_alpha), for parity tests and debugging. Stream-ordered.
@@ -103,19 +105,17 @@ int lgm_render_tile_lists(int B, int V, int N, int H, int W, const void *workspa
 int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
                            long long pair_capacity, int *n_contrib_out, float *final_T_out, void *stream);
 
-/* Diagnostics: while device_counters (a DEVICE uint64[8], caller-zeroed) is set, the render kernels add work
- * counts to it: [0] forward wavefront-entry iterations, [1] accepted (pixel, Gaussian) contributions,
+/* Diagnostics: when diag->render_counters (a DEVICE uint64 buffer, caller-zeroed) is set, that call's render kernels
+ * add work counts to it: [0] forward wavefront-entry iterations, [1] accepted (pixel, Gaussian) contributions,
  * [2] backward wavefront-entry iterations, [3] backward (pixel, Gaussian) gradient contributions,
  * [4] dense / [5] sparse wavefront reductions, [6] tile-list entries staged by the forward, [7] max forward
  * iterations of one wavefront; then 8 entries per tile t (B*V*T tiles): s_memrealtime stamps (100 MHz)
  * [8+8t] fwd start, [+1] fwd end, [+2], [+3] unused (the backward keeps per-work-item records), [+4] sort start,
  * [+5] sort end, and [+6] the tile's binned list length; then 8 entries per binning workgroup
- * (room for B*V*ceil(N/512); the binning launch uses its first B*ceil(V/3)*ceil(N/512)): phase stamps [0] start, [1] preprocessed, [2] tile tests done, [3] reserved, [4] end,
- * and [5] its binned pairs; then 4 entries per backward work item: start/end stamps, (entries | chunk << 20 |
- * tile << 40) and one unused -- so the buffer must hold 8 + 8*B*V*tiles + 8*B*V*ceil(N/512) +
- * 4*5*B*V*tiles entries.
- * NULL disables (default). Process-wide; not for concurrent use. */
-int lgm_render_debug_counters(unsigned long long *device_counters);
+ * (room for B*V*ceil(N/512); the binning launch uses its first B*ceil(V/3)*ceil(N/512)): phase stamps [0] start,
+ * [1] preprocessed, [2] tile tests done, [3] reserved, [4] end, and [5] its binned pairs; then 4 entries per backward
+ * work item: start/end stamps, (entries | chunk << 20 | tile << 40) and one unused -- so the buffer must hold
+ * 8 + 8*B*V*tiles + 8*B*V*ceil(N/512) + 4*5*B*V*tiles entries. */
 
 /* Per-call `options` of lgm_render_forward / lgm_render_backward (pass the same value to both).
  * LGM_RENDER_CLAMP_IMAGE: the forward writes clamp(image, 0, 1) (core/gs.py:87) and keeps a per-pixel mask in
@@ -136,11 +136,11 @@ int lgm_render_debug_counters(unsigned long long *device_counters);
 #define LGM_RENDER_DETERMINISTIC 16
 size_t lgm_render_workspace_size_opts(int B, int V, int N, int H, int W, long long pair_capacity, int options);
 
-/* Option flags (process-wide, default 0). LGM_RENDER_NO_CULL bins upstream's full 3-sigma tile rects instead of
- * dropping (Gaussian, tile) pairs where alpha < 1/255 is provable for every pixel; outputs are identical either
- * way (tests/test_render_gpu.py::test_exact_culling_is_output_preserving), only the work differs. */
+/* LGM_RENDER_NO_CULL: bin upstream's full 3-sigma tile rects instead of dropping (Gaussian, tile) pairs where
+ * alpha < 1/255 is provable for every pixel; outputs are identical either way
+ * (tests/test_render_gpu.py::test_exact_culling_is_output_preserving), only the work differs. A packed workspace for
+ * it needs lgm_render_count_pairs' pairs_out[1] (upstream's count) as its capacity. Per call, like every option. */
 #define LGM_RENDER_NO_CULL 1
-int lgm_render_set_flags(int flags);
 
 #ifdef __cplusplus
 }

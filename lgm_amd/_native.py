@@ -3,9 +3,14 @@
 There is no fallback: if the library is missing or cannot be loaded, every op raises. torch is imported first so
 that the library's NEEDED libamdhip64.so.7 resolves to the HIP runtime torch already loaded (same soname), giving
 one HIP runtime per process and letting device pointers and streams flow between torch and the library.
+
+The library holds no mutable global state besides its thread-local error string: diagnostics (the kernel profiler,
+the render work counters) travel with each call as an `lgm_diag` (include/lgm_common.h). The harness-side switch
+for them is `diagnostics(...)` here, whose value every wrapper passes as the call's `diag` (None = NULL).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -22,39 +27,36 @@ SIGNATURES = {
     "lgm_render_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_ll]),
     "lgm_render_workspace_size_opts": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_int]),
     "lgm_render_count_pairs": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_float, _c_float,
-                                        _c_float, _vp, _c_size, _vp, _vp]),
+                                        _c_float, _vp, _c_size, _vp, _vp, _vp]),
     "lgm_render_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_float,
-                                    _c_float, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _vp, _c_int, _vp]),
+                                    _c_float, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _vp, _c_int, _vp, _vp]),
     "lgm_render_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_float,
-                                     _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _c_int, _vp]),
+                                     _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _c_int, _vp, _vp]),
     "lgm_attn_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
-                                  _vp]),
+                                  _vp, _vp]),
     "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
-                                   _vp, _vp, _vp, _vp, _c_ll, _vp, _c_size, _vp]),
+                                   _vp, _vp, _vp, _vp, _c_ll, _vp, _c_size, _vp, _vp]),
     "lgm_attn_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "lgm_mva_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "lgm_mva_norm_tokens": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp,
-                                     _vp, _vp, _vp, _vp, _c_size, _vp]),
+                                     _vp, _vp, _vp, _vp, _c_size, _vp, _vp]),
     "lgm_mva_tokens_out": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _vp,
-                                    _vp]),
+                                    _vp, _vp]),
     "lgm_render_forward_loss": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float,
                                          _c_float, _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _c_int,
-                                         _vp]),
+                                         _vp, _vp]),
     "lgm_render_backward_loss": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float,
                                           _c_float, _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll,
-                                          _c_int, _vp]),
+                                          _c_int, _vp, _vp]),
     "lgm_render_tile_lists": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp,
                                        _vp]),
     "lgm_render_pixel_state": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp]),
     "lgm_gaussian_head_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp,
-                                           _c_size, _vp]),
+                                           _c_size, _vp, _vp]),
     "lgm_gaussian_head_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "lgm_gaussian_head_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                            _vp, _vp, _c_size, _vp]),
-    "lgm_render_debug_counters": (_c_int, [_vp]),
-    "lgm_render_set_flags": (_c_int, [_c_int]),
+                                            _vp, _vp, _c_size, _vp, _vp]),
     "lgm_profiler_create": (_vp, []),
-    "lgm_profiler_attach": (_c_int, [_vp]),
     "lgm_profiler_summary": (_c_int, [_vp, ctypes.c_char_p, _c_size]),
     "lgm_profiler_reset": (_c_int, [_vp]),
     "lgm_profiler_destroy": (None, [_vp]),
@@ -63,7 +65,8 @@ SIGNATURES = {
 _lib = None
 
 
-ABI_VERSION = 2
+ABI_VERSION = 3
+RENDER_NO_CULL = 1  # include/lgm_render.h LGM_RENDER_NO_CULL
 RENDER_CLAMP_IMAGE = 2  # include/lgm_render.h LGM_RENDER_CLAMP_IMAGE
 RENDER_BACKWARD_AGAIN = 4  # include/lgm_render.h LGM_RENDER_BACKWARD_AGAIN
 RENDER_DETERMINISTIC = 16  # include/lgm_render.h LGM_RENDER_DETERMINISTIC
@@ -111,19 +114,51 @@ def require_device_tensor(t: torch.Tensor, name: str):
                           "GPU-only too, core/gs.py:20)")
 
 
+class _Diag(ctypes.Structure):
+    """include/lgm_common.h lgm_diag."""
+    _fields_ = [("profiler", _vp), ("render_counters", _vp)]
+
+
+_diag_cur = None  # the lgm_diag every wrapper passes while a diagnostics() block is open (None: NULL)
+
+
+def diag():
+    """The `diag` argument for the next C-ABI call: NULL unless a diagnostics() block is open. (Harness state, not
+    library state: autograd runs the backward on its own thread, so a thread-local switch would miss it.)"""
+    return None if _diag_cur is None else ctypes.byref(_diag_cur)
+
+
+@contextlib.contextmanager
+def diagnostics(profiler=None, render_counters=None):
+    """Inside the block, every liblgm_amd call made through this package carries these diagnostics: a
+    KernelProfiler and/or a device uint64 tensor for the render work counters (include/lgm_render.h)."""
+    global _diag_cur
+    prev = _diag_cur
+    d = _Diag(profiler.h if profiler is not None else None,
+              render_counters.data_ptr() if render_counters is not None else None)
+    _diag_cur = d
+    try:
+        yield d
+    finally:
+        _diag_cur = prev
+
+
 class KernelProfiler:
-    """HIP events around every kernel liblgm_amd launches from this thread, on the launching stream
-    (include/lgm_common.h). summary() -> {kernel: (launches, total_ms)}."""
+    """HIP events around every kernel liblgm_amd launches (on the launching stream) while the profiler is entered
+    (`with prof:` = diagnostics(profiler=prof)). summary() -> {kernel: (launches, total_ms)}."""
 
     def __init__(self):
         self.h = lib().lgm_profiler_create()
+        self._cm = None
 
     def __enter__(self):
-        lib().lgm_profiler_attach(self.h)
+        self._cm = diagnostics(profiler=self)
+        self._cm.__enter__()
         return self
 
     def __exit__(self, *exc):
-        lib().lgm_profiler_attach(None)
+        cm, self._cm = self._cm, None
+        return cm.__exit__(*exc)
 
     def reset(self):
         lib().lgm_profiler_reset(self.h)

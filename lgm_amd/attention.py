@@ -47,7 +47,7 @@ class _PackedAttention(torch.autograd.Function):
             L_ = nat.lib()
             nat.check(L_.lgm_attn_forward(dt, B, L, H, D, float(scale), base, base + H * D * es,
                                           base + 2 * H * D * es, 3 * H * D, nat.ptr(o), nat.ptr(lse),
-                                          nat.stream_of(qkv.device)), "lgm_attn_forward")
+                                          nat.stream_of(qkv.device), nat.diag()), "lgm_attn_forward")
         ctx.save_for_backward(qkv, o, lse)
         ctx.scale = float(scale)
         return o
@@ -68,7 +68,7 @@ class _PackedAttention(torch.autograd.Function):
             nat.check(L_.lgm_attn_backward(dt, B, L, H, D, ctx.scale, base, base + hd, base + 2 * hd, 3 * H * D,
                                            nat.ptr(o), nat.ptr(lse), nat.ptr(d_o), dbase, dbase + hd,
                                            dbase + 2 * hd, 3 * H * D, nat.ptr(ws), ws_bytes,
-                                           nat.stream_of(qkv.device)), "lgm_attn_backward")
+                                           nat.stream_of(qkv.device), nat.diag()), "lgm_attn_backward")
         return d_qkv, None
 
 
@@ -164,7 +164,8 @@ class _NormTokens(torch.autograd.Function):
         ws = torch.empty(max(ws_bytes, 1), device=x.device, dtype=torch.uint8)
         nat.check(L_.lgm_mva_norm_tokens(_dtype_code(x), _dtype_code(tok), B, F, C, HW, groups, float(eps), nat.ptr(x),
                                          nat.ptr(w), nat.ptr(b), nat.ptr(tok), nat.ptr(mean), nat.ptr(rstd),
-                                         nat.ptr(ws), ws_bytes, nat.stream_of(x.device)), "lgm_mva_norm_tokens")
+                                         nat.ptr(ws), ws_bytes, nat.stream_of(x.device), nat.diag()),
+                  "lgm_mva_norm_tokens")
         ctx.save_for_backward(x, weight, mean, rstd)
         ctx.shape = (B, F, C, H, W, groups)
         return tok
@@ -198,7 +199,7 @@ class _TokensOut(torch.autograd.Function):
         r = None if res is None else res.contiguous()
         nat.check(nat.lib().lgm_mva_tokens_out(_dtype_code(y), 0 if r is None else _dtype_code(r), _dtype_code(out),
                                                B, F, C, H * W, nat.ptr(y), nat.ptr(r), float(skip), nat.ptr(out),
-                                               nat.stream_of(y.device)), "lgm_mva_tokens_out")
+                                               nat.stream_of(y.device), nat.diag()), "lgm_mva_tokens_out")
         ctx.meta = (B, F, C, H, W, float(skip), y.dtype, None if res is None else res.dtype)
         return out
 

@@ -38,7 +38,7 @@ def build(force: bool = False, verbose: bool = False, out: str = None, defines=(
     if out == OUT and not force and not needs_build():
         return OUT
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    objs = []
+    objs, cmds = [], []
     tag = "" if out == OUT else "." + os.path.basename(out)
     for src in sources():
         obj = os.path.join(HERE, "_lib", os.path.basename(src) + tag + ".o")
@@ -49,8 +49,14 @@ def build(force: bool = False, verbose: bool = False, out: str = None, defines=(
             [d if d.startswith("-") else f"-D{d}" for d in defines]  # A/B variants: defines or extra flags
         if verbose:
             print(" ".join(cmd))
-        subprocess.run(cmd, check=True)
+        cmds.append(cmd)
         objs.append(obj)
+    # the sources compile independently: in parallel (at most 8 at once: the container and the GPU box's share)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(8, len(cmds))) as ex:
+        for r in list(ex.map(lambda c: subprocess.run(c), cmds)):
+            if r.returncode:
+                raise subprocess.CalledProcessError(r.returncode, r.args)
     tmp = out + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
     os.replace(tmp, out)

@@ -952,8 +952,9 @@ size_t lgm_attn_workspace_size(int dtype, int B, int L, int H) {
 }
 
 int lgm_attn_forward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,
-                     const void *v, long long ld_qkv, void *o, float *lse, void *stream) {
+                     const void *v, long long ld_qkv, void *o, float *lse, void *stream, const lgm_diag *diag) {
     lgm::clear_error();
+    lgm::DiagScope ds(diag);
     int rc = lgm::attn::check(dtype, B, L, H, D);
     if (rc) return rc;
     if (!q || !k || !v || !o || !lse) {
@@ -966,8 +967,10 @@ int lgm_attn_forward(int dtype, int B, int L, int H, int D, float scale, const v
 
 int lgm_attn_backward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,
                       const void *v, long long ld_qkv, const void *o, const float *lse, const void *d_o, void *dq,
-                      void *dk, void *dv, long long ld_dqkv, void *workspace, size_t workspace_bytes, void *stream) {
+                      void *dk, void *dv, long long ld_dqkv, void *workspace, size_t workspace_bytes, void *stream,
+                      const lgm_diag *diag) {
     lgm::clear_error();
+    lgm::DiagScope ds(diag);
     int rc = lgm::attn::check(dtype, B, L, H, D);
     if (rc) return rc;
     if (!q || !k || !v || !o || !lse || !d_o || !dq || !dk || !dv) {

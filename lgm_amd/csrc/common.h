@@ -1,16 +1,29 @@
 // lgm_amd/csrc/common.h -- shared host-side helpers of liblgm_amd.so: thread-local error string, launch checks,
-// and the optional thread-local HIP-event kernel profiler (include/lgm_common.h) used by bench.py to time each
-// kernel on the stream it is launched on.
+// and the per-call diagnostics (include/lgm_common.h lgm_diag: the HIP-event kernel profiler bench.py uses to time
+// each kernel on the stream it is launched on).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+
+#include "lgm_common.h"
 
 namespace lgm {
 
 void set_error(const char *fmt, ...);
 void clear_error();
 
-// Kernel timing hooks: no-ops unless a profiler is attached to the calling thread.
+// The diagnostics of the entry point running on this thread: set for the duration of one call by a DiagScope at
+// its top (entry points run synchronously on the caller's thread and enqueue everything before returning), so
+// nothing outlives the call.
+struct DiagScope {
+    explicit DiagScope(const lgm_diag *d);
+    ~DiagScope();
+    DiagScope(const DiagScope &) = delete;
+    DiagScope &operator=(const DiagScope &) = delete;
+};
+const lgm_diag *call_diag();
+
+// Kernel timing hooks: no-ops unless the current call has a profiler.
 void prof_begin(const char *name, hipStream_t st);
 void prof_end(hipStream_t st);
 

@@ -1,10 +1,9 @@
-// lgm_amd/csrc/common.hip -- error string + thread-local HIP-event profiler (include/lgm_common.h).
+// lgm_amd/csrc/common.hip -- error string + the per-call HIP-event profiler (include/lgm_common.h).
 #include "common.h"
 
 #include <stdarg.h>
 #include <string.h>
 
-#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -30,7 +29,7 @@ struct lgm_profiler {
 
 namespace lgm {
 static thread_local char g_err[512] = {0};
-static std::atomic<lgm_profiler *> g_prof{nullptr};  // process-wide: autograd runs backward on its own thread
+static thread_local const lgm_diag *g_call_diag = nullptr;  // only while an entry point runs (DiagScope)
 static thread_local const char *g_pending = nullptr;
 static thread_local hipEvent_t g_pending_ev = nullptr;
 
@@ -42,8 +41,22 @@ void set_error(const char *fmt, ...) {
 }
 void clear_error() { g_err[0] = 0; }
 
+static thread_local int g_scope_depth = 0;
+DiagScope::DiagScope(const lgm_diag *d) {
+    if (g_scope_depth++ == 0) g_call_diag = d;  // (an entry point called from another keeps the outer call's)
+}
+DiagScope::~DiagScope() {
+    if (--g_scope_depth == 0) {
+        g_call_diag = nullptr;
+        g_pending_ev = nullptr;
+    }
+}
+const lgm_diag *call_diag() { return g_call_diag; }
+
+static lgm_profiler *call_profiler() { return g_call_diag ? g_call_diag->profiler : nullptr; }
+
 void prof_begin(const char *name, hipStream_t st) {
-    lgm_profiler *p = g_prof.load();
+    lgm_profiler *p = call_profiler();
     if (!p) return;
     std::lock_guard<std::mutex> lk(p->mu);
     g_pending = name;
@@ -51,7 +64,7 @@ void prof_begin(const char *name, hipStream_t st) {
     if (g_pending_ev) (void)hipEventRecord(g_pending_ev, st);
 }
 void prof_end(hipStream_t st) {
-    lgm_profiler *p = g_prof.load();
+    lgm_profiler *p = call_profiler();
     if (!p || !g_pending_ev) return;
     std::lock_guard<std::mutex> lk(p->mu);
     hipEvent_t b = p->get();
@@ -64,13 +77,9 @@ void prof_end(hipStream_t st) {
 
 extern "C" {
 const char *lgm_last_error(void) { return lgm::g_err; }
-int lgm_abi_version(void) { return 2; }
+int lgm_abi_version(void) { return 3; }
 
 lgm_profiler *lgm_profiler_create(void) { return new lgm_profiler(); }
-int lgm_profiler_attach(lgm_profiler *p) {
-    lgm::g_prof.store(p);
-    return LGM_OK;
-}
 int lgm_profiler_reset(lgm_profiler *p) {
     if (!p) return LGM_E_INVALID;
     std::lock_guard<std::mutex> lk(p->mu);
@@ -110,7 +119,6 @@ int lgm_profiler_summary(lgm_profiler *p, char *buf, size_t len) {
 }
 void lgm_profiler_destroy(lgm_profiler *p) {
     if (!p) return;
-    if (lgm::g_prof.load() == p) lgm::g_prof.store(nullptr);
     for (auto e : p->pool) (void)hipEventDestroy(e);
     delete p;
 }

@@ -309,8 +309,9 @@ size_t lgm_gaussian_head_workspace_size(int B, int V, int h, int w) {
 
 int lgm_gaussian_head_forward(int dtype, int B, int V, int h, int w, const void *x, const float *weight,
                               const float *bias, float *gaussians, float *rot_norm, void *workspace,
-                              size_t workspace_bytes, void *stream) {
+                              size_t workspace_bytes, void *stream, const lgm_diag *diag) {
     lgm::clear_error();
+    lgm::DiagScope ds(diag);
     int rc = lgm::check_head(dtype, B, V, h, w, x, weight);
     if (rc) return rc;
     if (B == 0) return LGM_OK;
@@ -339,8 +340,9 @@ int lgm_gaussian_head_forward(int dtype, int B, int V, int h, int w, const void 
 int lgm_gaussian_head_backward(int dtype, int B, int V, int h, int w, const void *x, const float *weight,
                                const float *bias, const float *rot_norm, const float *d_gaussians, void *dx,
                                float *d_weight, float *d_bias, void *workspace, size_t workspace_bytes,
-                               void *stream) {
+                               void *stream, const lgm_diag *diag) {
     lgm::clear_error();
+    lgm::DiagScope ds(diag);
     int rc = lgm::check_head(dtype, B, V, h, w, x, weight);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;

@@ -243,8 +243,10 @@ extern "C" size_t lgm_mva_workspace_size(int B, int F, int C, int HW, int groups
 
 extern "C" int lgm_mva_norm_tokens(int dtype_x, int dtype_tok, int B, int F, int C, int HW, int groups, float eps,
                                    const void *x, const float *gamma, const float *beta, void *tokens, float *mean,
-                                   float *rstd, void *workspace, size_t workspace_bytes, void *stream) {
+                                   float *rstd, void *workspace, size_t workspace_bytes, void *stream,
+                                   const lgm_diag *diag) {
     lgm::clear_error();
+    lgm::DiagScope ds(diag);
     if (B < 0 || F <= 0 || C <= 0 || HW < 0 || groups <= 0 || C % groups) {
         lgm::set_error("lgm_mva_norm_tokens: bad shape B=%d F=%d C=%d HW=%d groups=%d", B, F, C, HW, groups);
         return LGM_E_INVALID;
@@ -274,8 +276,10 @@ extern "C" int lgm_mva_norm_tokens(int dtype_x, int dtype_tok, int B, int F, int
 }
 
 extern "C" int lgm_mva_tokens_out(int dtype_y, int dtype_res, int dtype_out, int B, int F, int C, int HW,
-                                  const void *y, const void *res, float skip, void *out, void *stream) {
+                                  const void *y, const void *res, float skip, void *out, void *stream,
+                                  const lgm_diag *diag) {
     lgm::clear_error();
+    lgm::DiagScope ds(diag);
     if (B < 0 || F <= 0 || C <= 0 || HW < 0) {
         lgm::set_error("lgm_mva_tokens_out: bad shape B=%d F=%d C=%d HW=%d", B, F, C, HW);
         return LGM_E_INVALID;

@@ -8,10 +8,6 @@
 
 namespace {
 
-// Diagnostic work counters (lgm_render_debug_counters) and option flags (lgm_render_set_flags): process-wide.
-unsigned long long *g_counters = nullptr;
-int g_flags = 0;
-
 int check_common(int B, int V, int N, int H, int W, const void *g, const void *cv, const void *cvp, float tanx,
                  float tany, float mod, lgm::Dims &d) {
     if (B <= 0 || V <= 0 || N < 0 || H <= 0 || W <= 0 || H > lgm::BY * 65535 || W > lgm::BX * 65535) {
@@ -35,8 +31,8 @@ int check_common(int B, int V, int N, int H, int W, const void *g, const void *c
     d.fx = W / (2.0f * tanx);
     d.fy = H / (2.0f * tany);
     d.mod = mod;
-    d.counters = g_counters;
-    d.flags = g_flags;
+    const lgm_diag *diag = lgm::call_diag();  // this call's diagnostics (DiagScope), or none
+    d.counters = diag ? diag->render_counters : nullptr;
     d.options = 0;
     d.gt_img = d.gt_mask = nullptr;
     d.loss_part = d.loss_out = nullptr;
@@ -87,16 +83,6 @@ int check_ws(int B, int V, int N, int H, int W, const void *ws, size_t ws_bytes,
 
 extern "C" {
 
-int lgm_render_debug_counters(unsigned long long *device_counters) {
-    g_counters = device_counters;
-    return LGM_OK;
-}
-
-int lgm_render_set_flags(int flags) {
-    g_flags = flags;
-    return LGM_OK;
-}
-
 size_t lgm_render_workspace_size(int B, int V, int N, int H, int W, long long pair_capacity) {
     if (B <= 0 || V <= 0 || N < 0 || H <= 0 || W <= 0) return 0;
     return lgm::make_layout(B, V, N, H, W, pair_capacity).total;
@@ -109,8 +95,10 @@ size_t lgm_render_workspace_size_opts(int B, int V, int N, int H, int W, long lo
 
 int lgm_render_count_pairs(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
                            const float *cam_view_proj, float tanfovx, float tanfovy, float scale_modifier,
-                           void *workspace, size_t workspace_bytes, long long *pairs_out, void *stream) {
+                           void *workspace, size_t workspace_bytes, long long *pairs_out, void *stream,
+                           const lgm_diag *diag) {
     lgm::clear_error();
+    lgm::DiagScope ds(diag);
     lgm::Dims d;
     int rc = check_common(B, V, N, H, W, gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, scale_modifier, d);
     if (rc) return rc;
@@ -134,8 +122,9 @@ static int forward_impl(int B, int V, int N, int H, int W, const float *gaussian
                         float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
                         const float *gt_images, const float *gt_masks, float *loss_out, void *workspace,
                         size_t workspace_bytes, long long pair_capacity, long long *stats_out, int options,
-                        void *stream) {
+                        void *stream, const lgm_diag *diag) {
     lgm::clear_error();
+    lgm::DiagScope ds(diag);
     lgm::Dims d;
     int rc = check_common(B, V, N, H, W, gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, scale_modifier, d);
     if (rc) return rc;
@@ -178,8 +167,9 @@ static int backward_impl(int B, int V, int N, int H, int W, const float *gaussia
                          float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
                          const float *gt_images, const float *gt_masks, const float *d_loss, float *d_gaussians,
                          float *d_means2D, void *workspace, size_t workspace_bytes, long long pair_capacity,
-                         int options, void *stream) {
+                         int options, void *stream, const lgm_diag *diag) {
     lgm::clear_error();
+    lgm::DiagScope ds(diag);
     lgm::Dims d;
     int rc = check_common(B, V, N, H, W, gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, scale_modifier, d);
     if (rc) return rc;
@@ -214,24 +204,24 @@ int lgm_render_forward(int B, int V, int N, int H, int W, const float *gaussians
                        const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                        float scale_modifier, float *image, float *depth, float *alpha, int *radii_out,
                        void *workspace, size_t workspace_bytes, long long pair_capacity, long long *stats_out,
-                       int options, void *stream) {
+                       int options, void *stream, const lgm_diag *diag) {
     return forward_impl(B, V, N, H, W, gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, scale_modifier,
                         image, depth, alpha, radii_out, nullptr, nullptr, nullptr, workspace, workspace_bytes,
-                        pair_capacity, stats_out, options, stream);
+                        pair_capacity, stats_out, options, stream, diag);
 }
 
 int lgm_render_forward_loss(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
                             const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                             float scale_modifier, float *image, float *depth, float *alpha, const float *gt_images,
                             const float *gt_masks, float *loss_out, void *workspace, size_t workspace_bytes,
-                            long long pair_capacity, int options, void *stream) {
+                            long long pair_capacity, int options, void *stream, const lgm_diag *diag) {
     if (!gt_images || !gt_masks || !loss_out) {
         lgm::set_error("null gt_images / gt_masks / loss_out");
         return LGM_E_INVALID;
     }
     return forward_impl(B, V, N, H, W, gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, scale_modifier,
                         image, depth, alpha, nullptr, gt_images, gt_masks, loss_out, workspace, workspace_bytes,
-                        pair_capacity, nullptr, options, stream);
+                        pair_capacity, nullptr, options, stream, diag);
 }
 
 int lgm_render_backward_loss(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
@@ -239,14 +229,14 @@ int lgm_render_backward_loss(int B, int V, int N, int H, int W, const float *gau
                              float scale_modifier, const float *d_image, const float *d_alpha,
                              const float *gt_images, const float *gt_masks, const float *d_loss,
                              float *d_gaussians, void *workspace, size_t workspace_bytes, long long pair_capacity,
-                             int options, void *stream) {
+                             int options, void *stream, const lgm_diag *diag) {
     if (!gt_images || !gt_masks || !d_loss) {
         lgm::set_error("null gt_images / gt_masks / d_loss");
         return LGM_E_INVALID;
     }
     return backward_impl(B, V, N, H, W, gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, scale_modifier,
                          d_image, nullptr, d_alpha, gt_images, gt_masks, d_loss, d_gaussians, nullptr, workspace,
-                         workspace_bytes, pair_capacity, options, stream);
+                         workspace_bytes, pair_capacity, options, stream, diag);
 }
 
 int lgm_render_tile_lists(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
@@ -296,10 +286,10 @@ int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussian
                         const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,
                         float *d_gaussians, float *d_means2D, void *workspace, size_t workspace_bytes,
-                        long long pair_capacity, int options, void *stream) {
+                        long long pair_capacity, int options, void *stream, const lgm_diag *diag) {
     return backward_impl(B, V, N, H, W, gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, scale_modifier,
                          d_image, d_depth, d_alpha, nullptr, nullptr, nullptr, d_gaussians, d_means2D, workspace,
-                         workspace_bytes, pair_capacity, options, stream);
+                         workspace_bytes, pair_capacity, options, stream, diag);
 }
 
 }  // extern "C"

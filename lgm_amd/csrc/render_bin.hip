@@ -125,7 +125,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         return (MODE == EMIT_SLOT ? ((long long)bv * T + t) * slot_stride
                                   : (long long)tile_start[(size_t)bv * T + t]) + pos;
     };
-    // diagnostics: per-workgroup phase stamps after the per-tile records (see lgm_render_debug_counters)
+    // diagnostics: per-workgroup phase stamps after the per-tile records (see lgm_diag.render_counters)
     unsigned long long *stamp = d.counters ? d.counters + 8 + 8 * (size_t)d.BV * T +
                                              8 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x)
                                            : nullptr;
@@ -903,7 +903,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_
     int n;
     tile_range(tile, slot_stride, tile_start, tile_count, base, n);
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-    if (counters && threadIdx.x == 0) {  // per-workgroup timeline + bucket size (see lgm_render_debug_counters)
+    if (counters && threadIdx.x == 0) {  // per-workgroup timeline + bucket size (see lgm_diag.render_counters)
         counters[8 + 8 * (size_t)tile + 4] = t_start;
         counters[8 + 8 * (size_t)tile + 6] = (unsigned long long)n;
     }

@@ -79,9 +79,8 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
 struct Dims {
     int B, V, N, H, W, gx, gy, T, BV;
     float tanx, tany, fx, fy, mod;
-    unsigned long long *counters;  // optional device u64[8] work counters (see lgm_render_debug_counters), or null
-    int flags;                     // LGM_RENDER_NO_CULL: bin upstream's full 3-sigma rects (no exact culling)
-    int options;                   // per-call LGM_RENDER_CLAMP_IMAGE / LGM_RENDER_FUSED_LOSS
+    unsigned long long *counters;  // this call's device work counters (lgm_diag.render_counters), or null
+    int options;                   // per-call LGM_RENDER_* bits (NO_CULL, CLAMP_IMAGE, FUSED_LOSS, DETERMINISTIC)
     // LGM_RENDER_FUSED_LOSS (core/models.py:138-160): ground truth [BV,3,P] / [BV,P], the per-tile loss partials
     // (forward) and the gradients of the two MSE terms (backward)
     const float *gt_img, *gt_mask;
@@ -289,7 +288,7 @@ __device__ __forceinline__ bool preprocess_one(const float *g, const float *Vw, 
     o.x0 = x0; o.y0 = y0; o.x1 = x1; o.y1 = y1; o.radius = r;
     // --- exact opacity-aware cull of the emitted rect
     const float op = g[3];
-    if (d.flags & LGM_RENDER_NO_CULL) {
+    if (d.options & LGM_RENDER_NO_CULL) {
         o.hx = o.hy = 3.0e38f;
         o.tau = 3.0e38f;
         o.cx0 = x0; o.cx1 = x1; o.cy0 = y0; o.cy1 = y1;

@@ -889,7 +889,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             }
         }
     }
-    if (d.counters && tid == 0) {  // work-item timeline (lgm_render_debug_counters): start, end, (length | chunk | tile)
+    if (d.counters && tid == 0) {  // work-item timeline (lgm_diag.render_counters): start, end, (length | chunk | tile)
         unsigned long long *o = d.counters + item_stamps + 4 * (size_t)blockIdx.x;
         o[0] = t_item;
         o[1] = __builtin_amdgcn_s_memrealtime();

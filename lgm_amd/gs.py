@@ -58,9 +58,10 @@ class _RasterizeBatched(torch.autograd.Function):
             k = torch.zeros(2, dtype=torch.int64, device=dev)
             _native.check(L.lgm_render_count_pairs(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
                                                    _native.ptr(cam_view_proj), tanx, tany, scale_modifier,
-                                                   _native.ptr(ws), small, _native.ptr(k), stream),
+                                                   _native.ptr(ws), small, _native.ptr(k), stream, _native.diag()),
                           "lgm_render_count_pairs")
-            cap = max(int(k[0].item()), 1)  # pairs actually binned
+            # pairs actually binned (upstream's full count with LGM_RENDER_NO_CULL)
+            cap = max(int(k[1 if options & _native.RENDER_NO_CULL else 0].item()), 1)
             ws_bytes = L.lgm_render_workspace_size_opts(B, V, N, H, W, cap, options)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         image = torch.empty(B, V, 3, H, W, dtype=torch.float32, device=dev)
@@ -71,7 +72,8 @@ class _RasterizeBatched(torch.autograd.Function):
             _native.check(L.lgm_render_forward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
                                                _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
                                                _native.ptr(image), _native.ptr(depth), _native.ptr(alpha), None,
-                                               _native.ptr(ws), ws_bytes, cap, None, options, stream),
+                                               _native.ptr(ws), ws_bytes, cap, None, options, stream,
+                                               _native.diag()),
                           "lgm_render_forward")
         else:
             # (loss_mse, mse_image, mse_alpha, psnr) of core/models.py:145-148,167, computed by the kernels
@@ -81,7 +83,7 @@ class _RasterizeBatched(torch.autograd.Function):
                                                     scale_modifier, _native.ptr(image), _native.ptr(depth),
                                                     _native.ptr(alpha), _native.ptr(gt_img), _native.ptr(gt_mask),
                                                     _native.ptr(loss4), _native.ptr(ws), ws_bytes, cap, options,
-                                                    stream), "lgm_render_forward_loss")
+                                                    stream, _native.diag()), "lgm_render_forward_loss")
         # the workspace is saved like an input: autograd frees it after a (non-retain_graph) backward, so a training
         # loop that keeps the previous step's outputs alive does not hold two workspaces
         ctx.save_for_backward(g, cam_view, cam_view_proj, bg, ws, gt_img, gt_mask, loss4)
@@ -116,13 +118,13 @@ class _RasterizeBatched(torch.autograd.Function):
                                                      scale_modifier, _native.ptr(d_image), _native.ptr(d_alpha),
                                                      _native.ptr(gt_img), _native.ptr(gt_mask), _native.ptr(s2),
                                                      _native.ptr(d_g), _native.ptr(ws), ctx.ws_bytes, ctx.cap,
-                                                     bwd_options, stream), "lgm_render_backward_loss")
+                                                     bwd_options, stream, _native.diag()), "lgm_render_backward_loss")
         else:
             _native.check(L.lgm_render_backward(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
                                                 _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany, scale_modifier,
                                                 _native.ptr(d_image), _native.ptr(d_depth), _native.ptr(d_alpha),
                                                 _native.ptr(d_g), None, _native.ptr(ws), ctx.ws_bytes, ctx.cap,
-                                                bwd_options, stream), "lgm_render_backward")
+                                                bwd_options, stream, _native.diag()), "lgm_render_backward")
         return d_g, None, None, None, None, None, None, None, None, None, None, None
 
 
@@ -133,11 +135,12 @@ def deterministic_enabled() -> bool:
 
 
 def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, scale_modifier=1.0, clamp=False,
-              gt_images=None, gt_masks=None, deterministic=None):
+              gt_images=None, gt_masks=None, deterministic=None, no_cull=False):
     """Functional form: returns (image [B,V,3,H,W], depth [B,V,1,H,W], alpha [B,V,1,H,W]). The image is
     unclamped unless clamp=True, which applies core/gs.py:87's clamp(0, 1) (and its gradient) inside the kernels.
     With gt_images [B,V,3,H,W] and gt_masks [B,V,1,H,W] a 4th output (loss_mse, mse_image, mse_alpha, psnr) holds
-    LGM's training MSE terms (core/models.py:145-148,167), fused into the kernels; it is differentiable."""
+    LGM's training MSE terms (core/models.py:145-148,167), fused into the kernels; it is differentiable.
+    no_cull=True bins upstream's full 3-sigma tile rects (LGM_RENDER_NO_CULL: same outputs, more work)."""
     if not gaussians.is_cuda:  # CPU tensors: the torch path of BASELINE config 1 (lgm_amd/cpu.py), never the oracle
         from .cpu import render_cpu
         bgc = torch.as_tensor(bg, dtype=torch.float32).detach().cpu()
@@ -166,7 +169,7 @@ def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, sc
         gtm = gt_masks.to(dev, torch.float32).contiguous().detach()
         if tuple(gti.shape) != (B, V, 3, H, W) or tuple(gtm.shape) != (B, V, 1, H, W):
             raise ValueError("gt_images / gt_masks must be [B,V,3,H,W] / [B,V,1,H,W]")
-    options = _native.RENDER_CLAMP_IMAGE if clamp else 0
+    options = (_native.RENDER_CLAMP_IMAGE if clamp else 0) | (_native.RENDER_NO_CULL if no_cull else 0)
     if deterministic_enabled() if deterministic is None else deterministic:
         options |= _native.RENDER_DETERMINISTIC
     out = _RasterizeBatched.apply(g, cv, cvp, bgt, float(tanfovx), float(tanfovy), float(scale_modifier),
@@ -188,17 +191,20 @@ def count_pairs(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scal
     cvp = cam_view_proj.to(dev, torch.float32).contiguous()
     _native.check(L.lgm_render_count_pairs(B, V, N, H, W, _native.ptr(g), _native.ptr(cv), _native.ptr(cvp),
                                            float(tanfovx), float(tanfovy), float(scale_modifier), _native.ptr(ws),
-                                           small, _native.ptr(k), _native.stream_of(dev)), "lgm_render_count_pairs")
+                                           small, _native.ptr(k), _native.stream_of(dev), _native.diag()),
+                  "lgm_render_count_pairs")
     kk = k.tolist()
     return int(kk[0]), int(kk[1])
 
 
-def forward_state(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scale_modifier=1.0, lists=False):
+def forward_state(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scale_modifier=1.0, lists=False,
+                  no_cull=False):
     """Runs one forward and returns what it left in its workspace (numpy, one host sync), for parity tests and
     debugging -- the equivalent of reading upstream's saved buffers (radii, point_list/ranges, n_contrib):
       radii [B,V,N] int32; K_binned / K_reference (as count_pairs); tile_counts [B,V,T] int32;
       n_contrib, final_T [B,V,H,W]; with lists=True, ids[b][v] = the view's tile lists concatenated (tile-major,
-      each in compositing order)."""
+      each in compositing order). no_cull=True bins upstream's full 3-sigma rects (LGM_RENDER_NO_CULL)."""
+    options = _native.RENDER_NO_CULL if no_cull else 0
     L = _native.lib()
     g = gaussians.float().contiguous()
     dev = g.device
@@ -217,7 +223,8 @@ def forward_state(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, sc
     _native.check(L.lgm_render_forward(B, V, N, H, W, _native.ptr(g), _native.ptr(cv), _native.ptr(cvp),
                                        _native.ptr(bg), float(tanfovx), float(tanfovy), float(scale_modifier),
                                        _native.ptr(image), _native.ptr(depth), _native.ptr(alpha), _native.ptr(radii),
-                                       _native.ptr(ws), ws_bytes, 0, _native.ptr(stats), 0, stream),
+                                       _native.ptr(ws), ws_bytes, 0, _native.ptr(stats), options, stream,
+                                       _native.diag()),
                   "lgm_render_forward")
     T = _tiles(H, W)
     counts = torch.empty(B * V * T, dtype=torch.int32, device=dev)

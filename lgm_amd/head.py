@@ -43,7 +43,7 @@ class _Head(torch.autograd.Function):
         ws = torch.empty(max(ws_bytes, 1), device=x.device, dtype=torch.uint8)
         nat.check(L.lgm_gaussian_head_forward(_DT[x.dtype], B, V, h, w, nat.ptr(x), nat.ptr(W), nat.ptr(b),
                                               nat.ptr(out), nat.ptr(rot_norm), nat.ptr(ws), ws_bytes,
-                                              nat.stream_of(x.device)), "lgm_gaussian_head_forward")
+                                              nat.stream_of(x.device), nat.diag()), "lgm_gaussian_head_forward")
         ctx.save_for_backward(x, W, b if b is not None else W.new_empty(0), rot_norm)
         ctx.dims = (B, V, h, w, bias is not None, weight.shape, weight.dtype, None if bias is None else bias.dtype)
         return out
@@ -63,7 +63,7 @@ class _Head(torch.autograd.Function):
                                                nat.ptr(b) if has_bias else None, nat.ptr(rot_norm), nat.ptr(d_out),
                                                nat.ptr(dx),
                                                nat.ptr(dW), nat.ptr(db), nat.ptr(ws), ws_bytes,
-                                               nat.stream_of(x.device)), "lgm_gaussian_head_backward")
+                                               nat.stream_of(x.device), nat.diag()), "lgm_gaussian_head_backward")
         return dx, dW.reshape(wshape).to(wdtype), None if db is None else db.to(bdtype), None, None
 
 

@@ -23,10 +23,9 @@ for it in range(6):
     torch.cuda.synchronize()
     if it == 5:
         cnt.zero_()
-        L.lgm_render_debug_counters(_native.ptr(cnt))
-    torch.autograd.backward([o["image"], o["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
-    torch.cuda.synchronize()
-    L.lgm_render_debug_counters(None)
+    with _native.diagnostics(render_counters=cnt if it == 5 else None):
+        torch.autograd.backward([o["image"], o["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
+        torch.cuda.synchronize()
     g.grad = None
 c = cnt[:10].tolist()
 names = ["stage", "compact", "entries", "flush", "tail"]

@@ -1,4 +1,4 @@
-"""Work counters of one cfg3 forward+backward (lgm_render_debug_counters) -> gpurun_out/counters.json."""
+"""Work counters of one cfg3 forward+backward (lgm_diag.render_counters) -> gpurun_out/counters.json."""
 import json
 import os
 import sys
@@ -26,11 +26,10 @@ for _ in range(5):  # warm up (clocks, caches, code objects) before the instrume
     torch.autograd.backward([o["image"], o["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
     g.grad = None
 torch.cuda.synchronize()
-L.lgm_render_debug_counters(_native.ptr(cnt))
-out = r.render(g, cv, cvp, cp, bg_color=bg.to(dev))
-torch.autograd.backward([out["image"], out["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
-torch.cuda.synchronize()
-L.lgm_render_debug_counters(None)
+with _native.diagnostics(render_counters=cnt):
+    out = r.render(g, cv, cvp, cp, bg_color=bg.to(dev))
+    torch.autograd.backward([out["image"], out["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
+    torch.cuda.synchronize()
 c = cnt.tolist()
 names = ["fwd_wave_iters", "fwd_contribs", "bwd_wave_iters", "bwd_contribs", "bwd_dense", "bwd_sparse",
          "fwd_entries_staged", "fwd_max_wave_iters"]

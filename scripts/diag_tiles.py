@@ -22,10 +22,9 @@ cnt = torch.zeros(8 + 8 * M + 8 * NB + 4 * 5 * M + 32 * M, dtype=torch.int64, de
 L = _native.lib()
 r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev))
 torch.cuda.synchronize()
-L.lgm_render_debug_counters(_native.ptr(cnt))
-r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev))
-torch.cuda.synchronize()
-L.lgm_render_debug_counters(None)
+with _native.diagnostics(render_counters=cnt):
+    r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev))
+    torch.cuda.synchronize()
 tl = np.array(cnt[8: 8 + 8 * M].tolist(), dtype=np.int64).reshape(M, 8)
 n, staged = tl[:, 6], tl[:, 7]
 res = {"n_mean": float(n.mean()), "n_max": int(n.max()), "staged_mean": float(staged.mean()),

@@ -38,9 +38,26 @@ def test_workspace_and_errors():
     assert L.lgm_render_workspace_size(0, 6, 10, 256, 256, 0) == 0
     # invalid arguments are reported, never thrown
     rc = L.lgm_render_forward(1, 1, 10, 16, 16, None, None, None, None, 1.0, 1.0, 1.0, None, None, None, None, None,
-                              0, 0, None, 0, None)
+                              0, 0, None, 0, None, None)
     assert rc < 0 and b"null" in L.lgm_last_error()
     # attention: unsupported head dim / dtype are reported, never thrown
-    rc = L.lgm_attn_forward(1, 1, 16, 2, 48, 0.1, None, None, None, 0, None, None, None)
+    rc = L.lgm_attn_forward(1, 1, 16, 2, 48, 0.1, None, None, None, 0, None, None, None, None)
     assert rc < 0 and b"D must be" in L.lgm_last_error()
     assert L.lgm_attn_workspace_size(1, 2, 100, 4) == 2 * 100 * 4 * 4
+
+
+def test_no_process_wide_switches():
+    """no global mutable state besides the error string. The round-2 process-wide setters
+    (lgm_render_set_flags, lgm_render_debug_counters, lgm_profiler_attach) are gone: NO_CULL is a per-call option
+    bit and diagnostics a per-call lgm_diag; every compute entry point that takes a stream takes a diag after it
+    (the two workspace-inspection copies excepted)."""
+    from lgm_amd import build as B
+    B.build()
+    L = ctypes.CDLL(_native.LIB_PATH)
+    for gone in ("lgm_render_set_flags", "lgm_render_debug_counters", "lgm_profiler_attach"):
+        assert not hasattr(L, gone), gone
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        for name, args in re.findall(r"\b(lgm_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", txt):
+            if "void *stream" in args and name not in ("lgm_render_tile_lists", "lgm_render_pixel_state"):
+                assert args.rstrip().endswith("const lgm_diag *diag"), name

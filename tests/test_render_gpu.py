@@ -24,9 +24,9 @@ BWD_TOL = 1e-4
 GROUPS = {"mean": slice(0, 3), "opacity": slice(3, 4), "scale": slice(4, 7), "rot": slice(7, 11), "rgb": slice(11, 14)}
 
 
-def _run(cuda, g, cv, cvp, H, W, bg, mod=1.0, grads=None):
+def _run(cuda, g, cv, cvp, H, W, bg, mod=1.0, grads=None, no_cull=False):
     gd = g.to(cuda).requires_grad_(grads is not None)
-    img, dep, alp = rasterize(gd, cv.to(cuda), cvp.to(cuda), bg.to(cuda), TAN, TAN, H, W, mod)
+    img, dep, alp = rasterize(gd, cv.to(cuda), cvp.to(cuda), bg.to(cuda), TAN, TAN, H, W, mod, no_cull=no_cull)
     out = {"image": img.detach().cpu().numpy(), "depth": dep.detach().cpu().numpy(),
            "alpha": alp.detach().cpu().numpy()}
     if grads is not None:
@@ -194,15 +194,9 @@ def test_equal_depth_ties(cuda, oracle_mod, N):
 def test_exact_culling_is_output_preserving(cuda):
     """The exact opacity-aware tile culling drops only (Gaussian, tile) pairs that every pixel would skip: the
     forward is bitwise identical with and without it; gradients agree to float-atomic reordering."""
-    from lgm_amd import _native
     g, cv, cvp = scene(N=30000, V=2, seed=21)
     grads = upstream(1, 2, 128, 128)
-    L = _native.lib()
-    try:
-        L.lgm_render_set_flags(1)
-        full = _run(cuda, g, cv, cvp, 128, 128, grads[3], grads=grads[:3])
-    finally:
-        L.lgm_render_set_flags(0)
+    full = _run(cuda, g, cv, cvp, 128, 128, grads[3], grads=grads[:3], no_cull=True)  # per-call LGM_RENDER_NO_CULL
     culled = _run(cuda, g, cv, cvp, 128, 128, grads[3], grads=grads[:3])
     for k in ("image", "depth", "alpha"):
         assert np.array_equal(full[k], culled[k]), k

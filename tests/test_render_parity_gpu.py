@@ -198,12 +198,7 @@ def test_integer_parity_tile_lists(cuda, oracle_mod, name):
     product default): each GPU list is an in-order subsequence of the oracle's."""
     g, cv, cvp, H = _case(name)
     V = cv.shape[1]
-    L = _native.lib()
-    try:
-        L.lgm_render_set_flags(1)  # LGM_RENDER_NO_CULL
-        full = forward_state(g.to(cuda), cv.to(cuda), cvp.to(cuda), TAN, TAN, H, H, lists=True)
-    finally:
-        L.lgm_render_set_flags(0)
+    full = forward_state(g.to(cuda), cv.to(cuda), cvp.to(cuda), TAN, TAN, H, H, lists=True, no_cull=True)
     culled = forward_state(g.to(cuda), cv.to(cuda), cvp.to(cuda), TAN, TAN, H, H, lists=True)
     T = full["tile_counts"].shape[-1]
     nc_mismatch = 0

@@ -42,17 +42,34 @@ N_GAUSS, VIEWS, RES, POOL_SCENES = 100_000, 6, 256, 8
 POOL_SEED, CFG3_SEED, CFG2_SEED = 2, 1, 0
 
 
-def kernel_bytes(N, BV, K, P):
-    """SURVEY.md §8(d) algorithmic bytes per launch over BV renders: fwd = 56N + 60K + 20P, bwd = 112N + 84K + 28P
-    per view, K = upstream's num_rendered summed over the views (a build that culls more is still credited with
-    K_ref). k_bin (preprocess + emit) carries 56N + 8K per view, k_sort 8K."""
+def kernel_bytes(N, BV, K, P, B=None):
+    """SURVEY.md §8(d) algorithmic bytes per launch over BV renders of B scenes: fwd = 56N + 60K + 20P,
+    bwd = 112N + 84K + 28P per view, K = upstream's num_rendered summed over the views (a build that culls more is
+    still credited with K_ref). k_bin (preprocess + emit) carries 56N + 8K per view, k_sort 8K. k_preproc_bwd sums
+    a scene's views before the projection chain, so it is priced per SCENE: 112N (attributes in, 14 gradients out)
+    plus 32 B per (view, Gaussian) of accumulators and tile rects it reads -- the per-view 112N of §8(d) would credit
+    it with bytes it never moves (frac > 1)."""
+    B = BV if B is None else B
     return {
         "k_bin": 56 * N * BV + 8 * K,
         "k_sort": 8 * K,
         "k_render_fwd": 44 * K + 20 * P * BV,
         "k_render_bwd": 84 * K + 28 * P * BV,
-        "k_preproc_bwd": 112 * N * BV,
+        "k_preproc_bwd": 112 * N * B + 32 * N * BV,
     }
+
+
+def limiter_from_counters(rec, achieved_counter_gbs):
+    """What bounds a kernel, read off its PMC record (profiles/pmc_latest.json): HBM if the counted traffic runs at
+    >= 60 % of peak, VALU if the VALU pipe is busy >= 60 % of the wave cycles, else latency / issue (the waves wait)."""
+    if not rec:
+        return None
+    hbm = achieved_counter_gbs / PEAK_HBM_GBS if achieved_counter_gbs else 0.0
+    valu, wait = rec.get("valu_busy_frac", 0.0), rec.get("wait_frac", 0.0)
+    lds = rec.get("lds_bank_conflict_frac")
+    kind = "hbm" if hbm >= 0.6 else "valu" if valu >= 0.6 else "latency/issue"
+    return {"kind": kind, "hbm_frac_at_counter_bytes": round(hbm, 4), "valu_busy_frac": valu, "wait_frac": wait,
+            "lds_bank_conflict_frac": lds}
 
 
 def pmc_record(kernel):
@@ -65,12 +82,17 @@ def pmc_record(kernel):
         out = {"traffic": int(rec["hbm_read_bytes"] + rec["hbm_write_bytes"]),
                "traffic_source": f"profiles/pmc_latest.json ({d['_meta'].get('workload', '?')}, "
                                  f"commit {d['_meta'].get('commit', '?')})"}
-        lim = {k: rec[k] for k in ("wait_frac", "valu_busy_frac", "lds_bank_conflict_frac") if k in rec}
-        if lim:
-            out["counters"] = lim
+        out["counters"] = {k: rec[k] for k in ("wait_frac", "valu_busy_frac", "lds_bank_conflict_frac") if k in rec}
         return out
     except (OSError, KeyError, ValueError, TypeError):
         return {"traffic": None}
+
+
+def json_pmc(kernel):
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "pmc_latest.json")))[kernel]
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
 
 
 def host_cpu():
@@ -97,11 +119,11 @@ def cpu_baseline(g, cv, cvp, tan, bg, d_img, d_alpha, seconds):
     from oracle import oracle as O
     O.build()
     model, ncpu, share = host_cpu()
-    # nested OpenMP: `views` threads over the views x `tiles` threads over each view's tiles. Views first: the
-    # oracle's per-view binning and sort run on the view's thread, so fewer view threads leave cores idle there
-    # (on the 16-core share: 6 x 2 -> 0.66 Mpix/s, 2 x 8 -> 0.23 Mpix/s, profiles/r02)
+    # nested OpenMP: `views` threads over the views x `tiles` threads over each view's tiles, every core of the share
+    # busy (6 x 3 = 18 threads on a 16-core share: the per-view binning and sort run on the view's thread alone, so
+    # the tile threads idle through them; fewer view threads leave cores idle there: 2 x 8 -> 0.23 Mpix/s, profiles/r02)
     views = min(VIEWS, share)
-    tiles = max(1, share // views)
+    tiles = max(1, -(-share // views))
     args = (g.numpy(), cv.numpy(), cvp.numpy(), tan, RES, RES, bg.numpy())
     kw = dict(d_image=d_img.numpy(), d_alpha=d_alpha.numpy(), nthreads=views, tile_threads=tiles)
     O.render(*args, **kw)  # warm
@@ -112,10 +134,64 @@ def cpu_baseline(g, cv, cvp, tan, bg, d_img, d_alpha, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": round(reps * VIEWS * RES * RES / el / 1e6, 3), "unit": "Mpixels/s", "cores": views * tiles,
-            "kind": "port", "host_cpu": model, "host_cpus_visible": ncpu, "host_cpu_share": share,
+    return {"value": round(reps * VIEWS * RES * RES / el / 1e6, 3), "unit": "Mpixels/s", "cores": min(views * tiles,
+                                                                                                      share),
+            "threads": views * tiles, "kind": "port", "host_cpu": model, "host_cpus_visible": ncpu,
+            "host_cpu_share": share,
             "sample": f"oracle/raster_oracle.c fwd+bwd of the cfg3 scene (seed 1: 100k Gaussians x 6 views x 256^2),"
                       f" {reps} repetitions in {el:.1f} s, {views} threads over views x {tiles} over tiles"}
+
+
+def cpu_baseline_torch(g, cv, cvp, tan, bg, d_img, d_alpha):
+    """The product's own CPU path (lgm_amd/cpu.py: vectorised torch, autograd backward; what BASELINE config 1 runs)
+    on the same cfg3 scene, on every core of the share: fwd+bwd of ONE of its views (a bounded sample: the autograd
+    tape of one view already holds ~6 GB)."""
+    import torch
+
+    from lgm_amd.cpu import render_cpu
+    _, _, share = host_cpu()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(share)
+    try:
+        gg = g.clone().requires_grad_(True)
+        t0 = time.perf_counter()
+        img, _, alp = render_cpu(gg, cv[:, :1], cvp[:, :1], bg, tan, tan, RES, RES, clamp=True)
+        torch.autograd.backward([img, alp], [d_img[:, :1], d_alpha[:, :1]])
+        el = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": round(RES * RES / el / 1e6, 4), "unit": "Mpixels/s", "cores": share, "kind": "port",
+            "sample": f"lgm_amd/cpu.py render_cpu fwd+bwd (torch autograd) of view 0 of the cfg3 scene: {el:.1f} s"}
+
+
+def cpu_baseline_attention(seconds):
+    """the attention's CPU restatement (lgm_amd/cpu.py attention_cpu = the reference's fallback
+    Attention math, core/attention.py:51-64) at LGM's heaviest level for ONE object (L = 4096, 16 heads, D = 32,
+    fp32, fwd+bwd), on every core of the share; repetitions bounded by `seconds`."""
+    import torch
+
+    from lgm_amd.cpu import attention_cpu
+    _, _, share = host_cpu()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(share)
+    try:
+        L, H, D = 4096, 16, 32
+        qkv = torch.randn(1, L, 3, H, D, generator=torch.Generator().manual_seed(7)).requires_grad_(True)
+        d_o = torch.randn(1, L, H, D, generator=torch.Generator().manual_seed(8))
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            qkv.grad = None
+            attention_cpu(qkv, D ** -0.5).backward(d_o)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        torch.set_num_threads(prev)
+    flops = 14.0 * H * L * L * D * reps
+    return {"value": round(flops / el / 1e12, 4), "unit": "TFLOP/s", "cores": share, "kind": "port",
+            "ms_per_block": round(1e3 * el / reps, 1),
+            "sample": f"attention_cpu fwd+bwd, L=4096 H=16 D=32 fp32, 1 object: {reps} repetitions in {el:.1f} s"}
 
 
 def attention_bench(dev, steps: int = 10):
@@ -271,22 +347,19 @@ def cfg4_bench(dev, steps):
 CFG5_VIEWS, CFG5_PARAMS = 26, 415_000_000  # rendered views per object; the 'big' UNet's parameter count
 
 
-def cfg5_bench(dev, info, steps):
-    """The render side of BASELINE config 5 (main.py:82-109 training step, one object per GPU): the fused Gaussian
-    head (core/models.py:96-117) on a synthetic UNet output of 6 input views at splat 160 (N = 153,600), the render of
-    26 views at 512^2 with the training loss fused in (core/models.py:138-148), and the backward through both; then
-    the DDP gradient exchange of the UNet's 1.66 GB fp32 gradients (100 MB buckets, bf16 on the wire:
-    lgm_amd.dist.allreduce_bucketed) -- timed on its own, since the UNet itself is out of scope."""
+def cfg5_inputs(dev):
+    """BASELINE config 5's render-side inputs (seeded; shared with tests/test_training_gpu.py): the Gaussian head with
+    its conv set so that its Gaussians follow SURVEY §8(d)'s synthetic distribution (positions 0.35 x, scales
+    0.1 softplus(x - 2.2522): median 0.01) rather than a random-init conv's metre-scale splats, a synthetic UNet
+    output x [6, 14, 160, 160] (6 input views at splat 160 -> N = 153,600), 26 orbit cameras at -10 degrees, ground
+    truth images / masks at 512^2 and the random training background (core/models.py:135-138)."""
     import torch
 
     from lgm_amd import GaussianRenderer, Options
-    from lgm_amd import dist as D
     from lgm_amd.cameras import orbit_cameras
     from lgm_amd.head import GaussianHead
     gen = torch.Generator().manual_seed(5)
     head = GaussianHead().to(dev)
-    # the head's conv set so that its Gaussians follow SURVEY §8(d)'s synthetic distribution (positions 0.35 x,
-    # scales 0.1 softplus(x - 2.2522): median 0.01) rather than a random-init conv's metre-scale splats
     with torch.no_grad():
         head.conv.weight.copy_(torch.diag(torch.tensor([0.35] * 3 + [1.0] * 11)).view(14, 14, 1, 1))
         head.conv.bias.zero_()
@@ -296,7 +369,22 @@ def cfg5_bench(dev, info, steps):
     gt = torch.rand(1, CFG5_VIEWS, 3, 512, 512, generator=gen).to(dev)
     mask = (torch.rand(1, CFG5_VIEWS, 1, 512, 512, generator=gen) > 0.5).float().to(dev)
     bg = torch.rand(3, generator=gen).to(dev)
-    r = GaussianRenderer(Options(output_size=512))
+    return dict(head=head, x=x, cam_view=cv, cam_view_proj=cvp, cam_pos=cp, gt=gt, mask=mask, bg=bg,
+                renderer=GaussianRenderer(Options(output_size=512)))
+
+
+def cfg5_bench(dev, info, steps):
+    """The render side of BASELINE config 5 (main.py:82-109 training step, one object per GPU): the fused Gaussian
+    head (core/models.py:96-117) on a synthetic UNet output of 6 input views at splat 160 (N = 153,600), the render of
+    26 views at 512^2 with the training loss fused in (core/models.py:138-148), and the backward through both; then
+    the DDP gradient exchange of the UNet's 1.66 GB fp32 gradients (100 MB buckets, fp32 on the wire as the
+    reference's DDP: lgm_amd.dist.allreduce_bucketed) -- timed on its own, since the UNet itself is out of scope."""
+    import torch
+
+    from lgm_amd import dist as D
+    z = cfg5_inputs(dev)
+    head, x, cv, cvp, cp, gt, mask, bg, r = (z[k] for k in ("head", "x", "cam_view", "cam_view_proj", "cam_pos", "gt",
+                                                            "mask", "bg", "renderer"))
 
     def step():
         g = head(x, 1, 6)
@@ -312,8 +400,16 @@ def cfg5_bench(dev, info, steps):
 
     res = {"workload": "cfg5 render side (main.py:82-109, one object per GPU): Gaussian head (6 x 160^2 -> "
                        "153,600 Gaussians) + 26 views at 512^2 with the fused MSE loss, fwd+bwd; plus the DDP "
-                       "all-reduce of the UNet's 1.66 GB fp32 gradients (100 MB buckets, bf16 on the wire)",
+                       "all-reduce of the UNet's 1.66 GB fp32 gradients (100 MB buckets, fp32 on the wire)",
            "render_side_ms": round(timed(step, steps), 4)}
+    from lgm_amd import _native
+    prof = _native.KernelProfiler()  # per-kernel HIP-event times of the same step (a separate, untimed pass)
+    with prof:
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+    res["kernels"] = {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in prof.summary().items()}
+    prof.close()
     if info.world > 1:
         flat = torch.zeros(CFG5_PARAMS, device=dev)
         res["grad_allreduce_ms"] = round(timed(lambda: D.allreduce_bucketed(flat, 25_000_000, info), 3), 3)
@@ -374,10 +470,25 @@ def run(args):
     kern = prof.summary()
     prof.close()
 
+    # the same steps with bit-reproducible gradients (LGM_RENDER_DETERMINISTIC: int64 fixed-point accumulation,
+    # SURVEY §5.2), timed the same way: what making it the default would cost
+    det = None
+    if not args.no_det and not args.only_pool:  # (PMC runs: only the headline kernels, float atomics)
+        os.environ["LGM_AMD_DETERMINISTIC"] = "1"
+        try:
+            for _ in range(max(2, args.warmup // 2)):
+                step()
+            n_det = max(5, args.steps // 2)
+            el_det = D.timed_steps(step, n_det, info, torch.cuda.synchronize, dev)
+        finally:
+            os.environ["LGM_AMD_DETERMINISTIC"] = "0"
+        det = {"ms_per_step": round(1e3 * el_det / n_det, 4),
+               "Mpixels_per_s": round(POOL_SCENES * VIEWS * RES * RES * n_det / el_det / 1e6, 2), "steps": n_det}
+
     P = RES * RES
     pixels = POOL_SCENES * VIEWS * P * args.steps
     value = pixels / el / 1e6
-    kb = kernel_bytes(N_GAUSS, B * VIEWS, K, P)
+    kb = kernel_bytes(N_GAUSS, B * VIEWS, K, P, B)
     per_kernel = {k: {"avg_us": round(1e3 * ms / n, 2), "launches": n} for k, (n, ms) in kern.items()}
     ms_step = 1e3 * el / args.steps
     result = {
@@ -401,19 +512,30 @@ def run(args):
                    "pairs_binned_rank0": K_binned, "parallelism": f"scene-sharded x{world} (no collective)"},
         "kernels": per_kernel,
     }
+    if det:
+        det["slowdown_vs_float_atomics"] = round(det["ms_per_step"] / (1e3 * el / args.steps), 3)
+        result["deterministic"] = det
     if kern:
         dom = max(kern.items(), key=lambda kv: kv[1][1])[0]
         dom_avg_s = kern[dom][1] / kern[dom][0] / 1e3
         achieved = kb.get(dom, 0) / dom_avg_s / 1e9
-        binned = kernel_bytes(N_GAUSS, B * VIEWS, K_binned, P).get(dom, 0) / dom_avg_s / 1e9
+        binned = kernel_bytes(N_GAUSS, B * VIEWS, K_binned, P, B).get(dom, 0) / dom_avg_s / 1e9
         step_bytes = sum(kb.values())
+        pmc = pmc_record(dom)
+        counter_gbs = pmc["traffic"] / dom_avg_s / 1e9 if pmc.get("traffic") else None
+        # "bound" names the roofline the kernel is priced against (the render has no contraction: HBM, SURVEY
+        # §8(d)); what actually limits it is read off the counters ("limiter")
         result["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS,
                               "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                               "bytes_per_launch": kb.get(dom, 0),
                               "frac_at_binned_K": round(binned / PEAK_HBM_GBS, 4),
-                              "limiter": "latency / LDS issue, not HBM (see DESIGN.md §4: PMC wait, VALU and LDS "
-                                         "bank-conflict fractions)",
-                              **pmc_record(dom)}
+                              "frac_at_counter_bytes": round(counter_gbs / PEAK_HBM_GBS, 4) if counter_gbs else None,
+                              "limiter": limiter_from_counters(json_pmc(dom), counter_gbs),
+                              **pmc}
+        result["kernel_rooflines"] = {
+            k: {"avg_us": round(1e3 * ms / n, 2), "bytes": kb.get(k), "frac": round(kb[k] / (ms / n / 1e3) / 1e9 /
+                                                                                  PEAK_HBM_GBS, 4)}
+            for k, (n, ms) in kern.items() if k in kb}
         result["step_roofline"] = {"bytes": step_bytes, "achieved_GBs": round(step_bytes / (ms_step / 1e3) / 1e9, 2),
                                    "frac": round(step_bytes / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}
 
@@ -475,6 +597,12 @@ def run(args):
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(g3.detach().cpu(), cv[None], cvp[None], tan, bg3, d3_img, d3_alpha,
                                                   args.cpu_seconds)
+            result["cpu_baseline_torch"] = cpu_baseline_torch(g3.detach().cpu(), cv[None], cvp[None], tan, bg3,
+                                                              d3_img, d3_alpha)
+            result["cpu_baseline_attention"] = cpu_baseline_attention(min(5.0, args.cpu_seconds))
+            if "attention" in result:
+                result["attention"]["vs_cpu_restatement"] = round(
+                    result["attention"]["tflops"] / max(result["cpu_baseline_attention"]["value"], 1e-9), 1)
         print(json.dumps(result), flush=True)
     D.finalize(info)
 
@@ -494,6 +622,7 @@ def parse(argv=None):
     ap.add_argument("--no-attention", action="store_true", help="skip the secondary attention measurement")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 (LGM 'big') hot-path measurement")
     ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 (training step, render side) measurement")
+    ap.add_argument("--no-det", action="store_true", help="skip the deterministic-mode timing of the pool")
     ap.add_argument("--only-pool", action="store_true",
                     help="only the headline workload (for counter profiles: no other kernel launches of other sizes)")
     return ap.parse_args(argv)

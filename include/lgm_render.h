@@ -129,10 +129,12 @@ int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *worksp
 /* (internal) set by lgm_render_forward_loss / lgm_render_backward_loss; ignored in `options`. */
 #define LGM_RENDER_FUSED_LOSS 8
 /* LGM_RENDER_DETERMINISTIC: bit-reproducible gradients. The per-view gradient accumulators become
- * int64 fixed point (2^-32 units; integer atomics commute, so the sums do not depend on the order in which the
- * backward's work items finish) instead of fp32 float atomics. The forward is deterministic in either mode. The
- * workspace is larger: size it with lgm_render_workspace_size_opts(..., options). Pass it to forward and
- * backward alike. */
+ * int64 fixed point (integer atomics commute, so the sums do not depend on the order in which the backward's work
+ * items finish) instead of fp32 float atomics. The units follow the data: 2^-30 of the call's largest per-pixel
+ * seed |dL/dpixel| (found by one extra pass over the seeds), times per-(view, Gaussian) power-of-two normalisers of
+ * the screen-space mean and conic partials -- so a mean-MSE loss's ~1e-9 seeds keep full resolution and large
+ * footprints cannot overflow. The forward is deterministic in either mode. The workspace is larger: size it with
+ * lgm_render_workspace_size_opts(..., options). Pass it to forward and backward alike. */
 #define LGM_RENDER_DETERMINISTIC 16
 size_t lgm_render_workspace_size_opts(int B, int V, int N, int H, int W, long long pair_capacity, int options);
 

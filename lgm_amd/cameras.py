@@ -85,6 +85,32 @@ def tan_half_fov(fovy: float) -> float:
     return float(math.tan(0.5 * math.radians(fovy)))
 
 
+def get_rays(pose: torch.Tensor, h: int, w: int, fovy: float, opengl: bool = True):
+    """Per-pixel ray origins and unit directions [h, w, 3] of a c2w pose (core/utils.py:10-43; kiui's
+    safe_normalize: x / sqrt(max(x.x, 1e-20)))."""
+    x, y = torch.meshgrid(torch.arange(w, device=pose.device), torch.arange(h, device=pose.device), indexing="xy")
+    x, y = x.flatten(), y.flatten()
+    focal = h * 0.5 / np.tan(0.5 * np.deg2rad(fovy))
+    sgn = -1.0 if opengl else 1.0
+    dirs = torch.stack([(x - w * 0.5 + 0.5) / focal, (y - h * 0.5 + 0.5) / focal * sgn,
+                        torch.full_like(x, sgn, dtype=torch.float32)], -1).float()
+    rays_d = dirs @ pose[:3, :3].transpose(0, 1)
+    rays_o = pose[:3, 3].unsqueeze(0).expand_as(rays_d)
+    rays_d = rays_d / torch.sqrt(torch.clamp((rays_d * rays_d).sum(-1, keepdim=True), min=1e-20))
+    return rays_o.reshape(h, w, 3), rays_d.reshape(h, w, 3)
+
+
+def default_rays(input_size: int, fovy: float = 49.1, radius: float = 1.5, elevation: float = 0.0, device=None):
+    """LGM.prepare_default_rays (core/models.py:61-85): the Pluecker ray embeddings [4, 6, h, w] (cross(o, d), d)
+    of the 4 input views at azimuths 0 / 90 / 180 / 270."""
+    out = []
+    for az in (0, 90, 180, 270):
+        pose = torch.from_numpy(orbit_camera(elevation, az, radius=radius))
+        o, d = get_rays(pose, input_size, input_size, fovy)
+        out.append(torch.cat([torch.cross(o, d, dim=-1), d], dim=-1))
+    return torch.stack(out, 0).permute(0, 3, 1, 2).contiguous().to(device)
+
+
 def orbit_cameras_batched(elevation, azimuth, radius: float = 1.5, fovy: float = 49.1, znear: float = 0.5,
                           zfar: float = 2.5, device=None):
     """Device-side batched camera build for the orbit video loops of infer.py:132-145 / app.py:
@@ -114,15 +140,25 @@ def orbit_cameras_batched(elevation, azimuth, radius: float = 1.5, fovy: float =
 
 
 def render_orbit_frames(renderer, gaussians, azimuths, elevation: float = 0.0, radius: float = 1.5,
-                        scale_modifier: float = 1.0, chunk: int = 60):
-    """infer.py:132-145's video loop (one render per azimuth) as batched renders of `chunk` views each, with the
-    cameras built on the device: returns uint8 frames [V, H, W, 3] (on the renderer's device)."""
+                        scale_modifier=1.0, chunk: int = 60):
+    """infer.py:114-145's video loops (one render per azimuth) as batched renders of up to `chunk` views each, with
+    the cameras built on the device: returns uint8 frames [V, H, W, 3] (on the renderer's device), each
+    (image * 255) truncated as the reference's .astype(np.uint8). scale_modifier: one float, or one per azimuth
+    (infer.py's fancy_video renders azimuth a with min(a / 360, 1), :129-131); consecutive frames with the same
+    scale share a call."""
     opt = renderer.opt
     dev = gaussians.device
     cv, cvp, cp = orbit_cameras_batched(elevation, azimuths, radius, opt.fovy, opt.znear, opt.zfar, device=dev)
+    V = cv.shape[0]
+    sm = np.broadcast_to(np.asarray(scale_modifier, dtype=np.float64), (V,))
     frames = []
-    for v0 in range(0, cv.shape[0], chunk):
-        img = renderer.render(gaussians, cv[None, v0:v0 + chunk], cvp[None, v0:v0 + chunk], cp[None, v0:v0 + chunk],
-                              scale_modifier=scale_modifier)["image"][0]
+    v0 = 0
+    while v0 < V:
+        v1 = v0 + 1
+        while v1 < V and v1 - v0 < chunk and sm[v1] == sm[v0]:
+            v1 += 1
+        img = renderer.render(gaussians, cv[None, v0:v1], cvp[None, v0:v1], cp[None, v0:v1],
+                              scale_modifier=float(sm[v0]))["image"][0]
         frames.append((img.permute(0, 2, 3, 1) * 255).to(torch.uint8))
+        v0 = v1
     return torch.cat(frames, 0)

@@ -18,8 +18,6 @@ upstream's backward does).
 """
 from __future__ import annotations
 
-import math
-
 import torch
 
 BLOCK = 16
@@ -210,4 +208,4 @@ def gaussian_head_cpu(x, weight, bias, B: int, V: int):
                       F.normalize(y[..., 7:11]), 0.5 * torch.tanh(y[..., 11:]) + 0.5], dim=-1)
 
 
-__all__ = ["render_cpu", "attention_cpu", "gaussian_head_cpu", "math"]
+__all__ = ["render_cpu", "attention_cpu", "gaussian_head_cpu"]

@@ -26,7 +26,6 @@ __host__ __device__ __forceinline__ size_t acc_index(int q, size_t bvN_i, size_t
 inline size_t acc_elems(size_t B, size_t V, size_t N) { return B * V * N * NACC_V + B * N * NACC_S; }
 constexpr int LDS_HIST_MAX = 8192;                   // tiles per view for the LDS-histogram binning path
 constexpr float LOG2E = 1.4426950408889634f;
-constexpr float DET_SCALE = 4294967296.0f;  // 2^32: deterministic-mode fixed-point units per 1.0
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -36,14 +35,15 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 //   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
 struct Layout {
     size_t gP, gQ, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, wlast, cfin, ck, cklist, nck, cmask,
-        accum, lossp, misc, total;
+        accum, lossp, lossw, misc, total;
     long long cap;
     int ck_region;  // backward checkpoint slots per region (8 regions; the forward shards tiles over them)
     bool slot;
 };
 
-// det (LGM_RENDER_DETERMINISTIC): the per-view gradient accumulators are int64 fixed point (2^-32 units) instead of
-// fp32: integer atomics commute, so the backward's sums do not depend on the order of its work items.
+// det (LGM_RENDER_DETERMINISTIC): the per-view gradient accumulators are int64 fixed point (data-scaled units, see
+// render_raster.hip det_norm) instead of fp32: integer atomics commute, so the backward's sums do not depend on the
+// order of its work items.
 inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capacity, bool det = false) {
     const size_t BV = (size_t)B * V, T = (size_t)((W + BX - 1) / BX) * ((H + BY - 1) / BY), P = (size_t)H * W;
     Layout L;
@@ -56,7 +56,8 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.rects = take(BV * N * 8);
     L.tile_count = take(BV * T * 4);
     L.misc = take(64);  // right after tile_count: the binning clears both with one memset (u64 [0..1]: pair
-                        // counts of k_bin; u32 [4..11]: the backward-checkpoint region counters)
+                        // counts of k_bin; u32 [4..11]: the backward-checkpoint region counters; u32 [12]: the
+                        // fused loss reduction's arrival counter; u32 [13]: deterministic mode's max |dL/dpixel|)
     L.tile_start = take((BV * T + 1) * 4);
     L.order = take(BV * T * 4);
     L.pairs = take((size_t)L.cap * 8);
@@ -72,6 +73,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.cmask = take(BV * P);
     L.accum = take(acc_elems(B, V, N) * (det ? 8 : 4));
     L.lossp = take(BV * T * 2 * 4);  // per-tile sums of squared image / alpha residuals (fused loss)
+    L.lossw = take(((BV * T + 2047) / 2048) * 16);  // their per-workgroup double2 partials (k_loss_reduce)
     L.total = o;
     return L;
 }

@@ -446,33 +446,70 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     }
 }
 
-// Fused loss, final reduction over the per-tile partials (one workgroup, fixed order):
+// Fused loss, final reduction over the per-tile (image, alpha) partials, fixed order, one launch: workgroup g sums
+// tiles [g * LR_TILES, +LR_TILES) (each thread LR_PER independent loads, then a fixed tree), writes its double2
+// partial, and the workgroup that arrives last (a counter in the workspace, zeroed by the forward's binning and
+// reset by that workgroup) sums the partials in workgroup order and writes
 // out = (loss_mse, mse_image, mse_alpha, psnr) as core/models.py:148 (F.mse_loss twice) and :167 (psnr).
-__global__ __launch_bounds__(256) void k_loss_reduce(int M, const float *__restrict__ part, double n_img, double n_a,
-                                                     float *__restrict__ out) {
-    __shared__ double s[2][256];
-    const int t = threadIdx.x;
+// (Was one workgroup looping over every tile: 38.8 us at cfg5's 26,624 tiles, now a few us.)
+constexpr int LR_THREADS = 256, LR_PER = 8, LR_TILES = LR_THREADS * LR_PER;
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__global__ __launch_bounds__(LR_THREADS) void k_loss_reduce(int M, const float2 *__restrict__ part, double n_img,
+                                                           double n_a, double2 *__restrict__ wg_part,
+                                                           unsigned *__restrict__ counter, float *__restrict__ out) {
+    __shared__ double s[2][LR_THREADS / 64];
+    __shared__ bool s_last;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int k0 = blockIdx.x * LR_TILES + t;
+    float2 v[LR_PER];
+#pragma unroll
+    for (int u = 0; u < LR_PER; u++) {
+        const int k = k0 + u * LR_THREADS;
+        v[u] = k < M ? part[k] : make_float2(0.f, 0.f);
+    }
     double a = 0.0, b = 0.0;
-    for (int k = t; k < M; k += 256) {
-        a += part[2 * (size_t)k];
-        b += part[2 * (size_t)k + 1];
+#pragma unroll
+    for (int u = 0; u < LR_PER; u++) {
+        a += (double)v[u].x;
+        b += (double)v[u].y;
     }
-    s[0][t] = a;
-    s[1][t] = b;
+    a = wave_sum_f64(a);
+    b = wave_sum_f64(b);
+    if (lane == 0) { s[0][w] = a; s[1][w] = b; }
     __syncthreads();
-    for (int h = 128; h > 0; h >>= 1) {
-        if (t < h) {
-            s[0][t] += s[0][t + h];
-            s[1][t] += s[1][t + h];
-        }
-        __syncthreads();
-    }
     if (t == 0) {
-        const float mi = (float)(s[0][0] / n_img), ma = (float)(s[1][0] / n_a);
+        double2 r = make_double2(0.0, 0.0);
+        for (int q = 0; q < LR_THREADS / 64; q++) { r.x += s[0][q]; r.y += s[1][q]; }
+        wg_part[blockIdx.x] = r;
+        __threadfence();  // the partial is visible device-wide before the arrival is counted
+        s_last = atomicAdd(counter, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // acquire: the other workgroups' partials (written back from their XCDs' L2s)
+    double2 r = make_double2(0.0, 0.0);  // the last workgroup: partials in workgroup order (lanes, then a tree)
+    for (int g = t; g < (int)gridDim.x; g += LR_THREADS) {
+        const double2 x = wg_part[g];
+        r.x += x.x;
+        r.y += x.y;
+    }
+    r.x = wave_sum_f64(r.x);
+    r.y = wave_sum_f64(r.y);
+    if (lane == 0) { s[0][w] = r.x; s[1][w] = r.y; }
+    __syncthreads();
+    if (t == 0) {
+        double si = 0.0, sa = 0.0;
+        for (int q = 0; q < LR_THREADS / 64; q++) { si += s[0][q]; sa += s[1][q]; }
+        const float mi = (float)(si / n_img), ma = (float)(sa / n_a);
         out[0] = mi + ma;
         out[1] = mi;
         out[2] = ma;
         out[3] = -10.f * log10f(mi);
+        *counter = 0u;  // ready for the next launch on this workspace
     }
 }
 
@@ -485,6 +522,128 @@ __device__ __forceinline__ float row_sum16(float v) {
     LGM_DPP_ADD(v, 0x141);  // row_half_mirror
     LGM_DPP_ADD(v, 0x140);  // row_mirror
     return v;
+}
+
+// The per-pixel seeds of the backward: dL/dpixel (colour, depth, alpha) after the fused loss's MSE terms and the
+// clamp's gradient mask, and the forward's pre-background totals. Shared by k_render_bwd and (deterministic mode)
+// k_det_seed_max, so both see the same values.
+struct PixelSeed {
+    float dp0, dp1, dp2, dpd, dpa;
+    float4 cf;
+};
+template <bool DEPTH, bool LOSS>
+__device__ __forceinline__ void pixel_seed(const Dims &d, bool inside, int bv, size_t P, size_t pid, float T_final,
+                                           const float *__restrict__ bg, const float4 *__restrict__ cfin,
+                                           const float *__restrict__ d_img, const float *__restrict__ d_depth,
+                                           const float *__restrict__ d_alpha, const unsigned char *__restrict__ cmask,
+                                           PixelSeed &o) {
+    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, dpd = 0.f, dpa = 0.f;
+    float4 cf = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (inside) {
+        cf = cfin[bv * P + pid];
+        if (d_img) {
+            const float *di = d_img + (size_t)bv * 3 * P;
+            dp0 = di[pid];
+            dp1 = di[P + pid];
+            dp2 = di[2 * P + pid];
+        }
+        if (LOSS) {
+            // the MSE seeds (core/models.py:148): dL/dimage += 2 (image - gt) dL/dmse_image / numel, likewise alpha;
+            // image recomputed from the forward's totals exactly as the forward formed it
+            const float s_img = 2.f * d.d_loss[0] / (float)(3.0 * d.BV * (double)P);
+            const float s_a = 2.f * d.d_loss[1] / (float)((double)d.BV * P);
+            const float m = d.gt_mask[bv * P + pid];
+            const float *gi = d.gt_img + (size_t)bv * 3 * P;
+            float c0 = fmaf(T_final, bg[0], cf.x), c1 = fmaf(T_final, bg[1], cf.y), c2 = fmaf(T_final, bg[2], cf.z);
+            if (d.options & LGM_RENDER_CLAMP_IMAGE) {
+                c0 = fminf(fmaxf(c0, 0.f), 1.f);
+                c1 = fminf(fmaxf(c1, 0.f), 1.f);
+                c2 = fminf(fmaxf(c2, 0.f), 1.f);
+            }
+            dp0 += s_img * (c0 - (gi[pid] * m + bg[0] * (1.f - m)));
+            dp1 += s_img * (c1 - (gi[P + pid] * m + bg[1] * (1.f - m)));
+            dp2 += s_img * (c2 - (gi[2 * P + pid] * m + bg[2] * (1.f - m)));
+            dpa = s_a * ((1 - T_final) - m);
+        }
+        if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // torch clamp gradient: passes where 0 <= x <= 1
+            const unsigned m = cmask[bv * P + pid];
+            dp0 = (m & 1u) ? dp0 : 0.f;
+            dp1 = (m & 2u) ? dp1 : 0.f;
+            dp2 = (m & 4u) ? dp2 : 0.f;
+        }
+        if (DEPTH) dpd = d_depth[bv * P + pid];
+        if (d_alpha) dpa += d_alpha[bv * P + pid];
+    }
+    o.dp0 = dp0; o.dp1 = dp1; o.dp2 = dp2; o.dpd = dpd; o.dpa = dpa;
+    o.cf = cf;
+}
+
+// ---- Deterministic mode (LGM_RENDER_DETERMINISTIC): int64 fixed-point accumulators with scales that follow the
+// data, so neither tiny nor huge gradients lose their meaning.
+//  * a per-call scale 2^s with s = DET_BITS - exponent(max |dL/dpixel| over every seed): the accumulators' unit is
+//    2^-DET_BITS of the largest per-pixel seed, whatever the loss normalisation (LGM's mean-MSE gives dL/dpixel
+//    ~1e-9 at 8 x 8 views of 512^2: a fixed 2^-32 unit would leave its partials only tens of units);
+//  * per (view, Gaussian) power-of-two normalisers of the view-dependent partials, from the compositing record (so
+//    k_render_bwd and k_preproc_bwd derive bitwise the same exponents): dL/dmean2D by (W/2) sqrt(A) (resp. (H/2)
+//    sqrt(C)) and dL/dconic by 1 / Sigma_xx, 1 / sqrt(Sigma_xx Sigma_yy), 1 / Sigma_yy (Sigma = conic^-1): with
+//    alpha >= 1/255 only where q <= 2 ln 255, each normalised per-pixel term is bounded by a small constant times
+//    |dL/dG|, so a large, elongated Gaussian's conic partials (pixel offsets of hundreds) cannot overflow int64 and a
+//    small one's keep their resolution.
+// Every power-of-two scaling is exact, so the only rounding is each flush's conversion to an integer (nearest).
+constexpr int DET_BITS = 30;  // seed max -> 2^30 units: per flush |value| <= ~2^51, sums of 2^11 flushes < 2^63
+__device__ __forceinline__ int f32_exp(float x) { return (int)((__float_as_uint(x) >> 23) & 0xffu) - 127; }
+__device__ __forceinline__ int det_seed_shift(const unsigned *det_max) {  // s: the call's global scale exponent
+    const float m = __uint_as_float(*det_max);
+    return (m > 0.f && m < 3.0e38f) ? DET_BITS - f32_exp(m) : 0;
+}
+struct DetNorm {
+    int k[6];  // exponents of the view record's slots: mean2D x, y, conic A, B, C, depth
+};
+__device__ __forceinline__ DetNorm det_norm(float Ap, float Bp, float Cp, int W, int H) {
+#pragma clang fp contract(off)
+    DetNorm n;
+    const float detp = Ap * Cp - 0.25f * (Bp * Bp);  // KQ^2 det(conic): the record holds -KQ A, -2 KQ B, -KQ C
+    if (!(detp > 0.f) || !(detp < 3.0e38f) || !(Ap < 0.f) || !(Cp < 0.f)) {
+        for (int q = 0; q < 6; q++) n.k[q] = 0;
+        return n;
+    }
+    const int ea = f32_exp(-Ap), ec = f32_exp(-Cp), ed = f32_exp(detp);
+    auto cl = [](int x) { return min(60, max(-60, x)); };
+    n.k[0] = cl(-(f32_exp(0.5f * (float)W) + (ea >> 1)));
+    n.k[1] = cl(-(f32_exp(0.5f * (float)H) + (ec >> 1)));
+    n.k[2] = cl(ed - ec);              // 1 / Sigma_xx ~ det / C
+    n.k[3] = cl(ed - ((ea + ec) >> 1));  // 1 / sqrt(Sigma_xx Sigma_yy)
+    n.k[4] = cl(ed - ea);              // 1 / Sigma_yy ~ det / A
+    n.k[5] = 0;
+    return n;
+}
+
+// k_det_seed_max: grid (B*V*T), block 256: max |dL/dpixel| over every seed of the call -> *det_max (float bits,
+// atomicMax on the non-negative bit pattern; zeroed by the caller).
+template <bool DEPTH, bool LOSS>
+__global__ __launch_bounds__(256) void k_det_seed_max(Dims d, const float *__restrict__ final_T,
+                                                      const float *__restrict__ bg, const float4 *__restrict__ cfin,
+                                                      const float *__restrict__ d_img, const float *__restrict__ d_depth,
+                                                      const float *__restrict__ d_alpha,
+                                                      const unsigned char *__restrict__ cmask,
+                                                      unsigned *__restrict__ det_max) {
+    const int tile = blockIdx.x;
+    const int bv = tile / d.T, t = tile - bv * d.T;
+    const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
+    int lx, ly;
+    tile_pixel(threadIdx.x, lx, ly);
+    const int px = tx0 + lx, py = ty0 + ly;
+    const bool inside = px < d.W && py < d.H;
+    const size_t P = (size_t)d.H * d.W;
+    const size_t pid = inside ? (size_t)d.W * py + px : 0;
+    PixelSeed sd;
+    pixel_seed<DEPTH, LOSS>(d, inside, bv, P, pid, inside ? final_T[bv * P + pid] : 0.f, bg, cfin, d_img, d_depth,
+                            d_alpha, cmask, sd);
+    float m = fmaxf(fmaxf(fabsf(sd.dp0), fabsf(sd.dp1)), fmaxf(fmaxf(fabsf(sd.dp2), fabsf(sd.dpd)), fabsf(sd.dpa)));
+    unsigned mb = __float_as_uint(m);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o, 64));
+    if ((threadIdx.x & 63) == 0 && mb) atomicMax(det_max, mb);
 }
 
 // k_render_bwd: grid (B*V*T + CK slots), block 256. DEPTH: an upstream depth gradient is present (LGM passes none).
@@ -520,7 +679,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const int *__restrict__ nck,
     const unsigned *__restrict__ ckctr, int ck_region, const float *__restrict__ d_img,
     const float *__restrict__ d_depth, const float *__restrict__ d_alpha, const unsigned char *__restrict__ cmask,
-    float *__restrict__ accum, long long item_stamps) {
+    float *__restrict__ accum, const unsigned *__restrict__ det_max, long long item_stamps) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
     constexpr int CH = BWD_CHUNK, LS = CH + 1;  // entries per staged chunk; padded LDS row stride
     __shared__ StageBwd S;
@@ -575,43 +734,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const size_t pid = inside ? (size_t)d.W * py + px : 0;
     const float T_final = inside ? final_T[bv * P + pid] : 0.f;
     const int last = inside ? n_contrib[bv * P + pid] : 0;
-    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, dpd = 0.f, dpa = 0.f;
-    float4 cf = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (inside) {
-        cf = cfin[bv * P + pid];
-        if (d_img) {
-            const float *di = d_img + (size_t)bv * 3 * P;
-            dp0 = di[pid];
-            dp1 = di[P + pid];
-            dp2 = di[2 * P + pid];
-        }
-        if (LOSS) {
-            // the MSE seeds (core/models.py:148): dL/dimage += 2 (image - gt) dL/dmse_image / numel, likewise alpha;
-            // image recomputed from the forward's totals exactly as the forward formed it
-            const float s_img = 2.f * d.d_loss[0] / (float)(3.0 * d.BV * (double)P);
-            const float s_a = 2.f * d.d_loss[1] / (float)((double)d.BV * P);
-            const float m = d.gt_mask[bv * P + pid];
-            const float *gi = d.gt_img + (size_t)bv * 3 * P;
-            float c0 = fmaf(T_final, bg[0], cf.x), c1 = fmaf(T_final, bg[1], cf.y), c2 = fmaf(T_final, bg[2], cf.z);
-            if (d.options & LGM_RENDER_CLAMP_IMAGE) {
-                c0 = fminf(fmaxf(c0, 0.f), 1.f);
-                c1 = fminf(fmaxf(c1, 0.f), 1.f);
-                c2 = fminf(fmaxf(c2, 0.f), 1.f);
-            }
-            dp0 += s_img * (c0 - (gi[pid] * m + bg[0] * (1.f - m)));
-            dp1 += s_img * (c1 - (gi[P + pid] * m + bg[1] * (1.f - m)));
-            dp2 += s_img * (c2 - (gi[2 * P + pid] * m + bg[2] * (1.f - m)));
-            dpa = s_a * ((1 - T_final) - m);
-        }
-        if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // torch clamp gradient: passes where 0 <= x <= 1
-            const unsigned m = cmask[bv * P + pid];
-            dp0 = (m & 1u) ? dp0 : 0.f;
-            dp1 = (m & 2u) ? dp1 : 0.f;
-            dp2 = (m & 4u) ? dp2 : 0.f;
-        }
-        if (DEPTH) dpd = d_depth[bv * P + pid];
-        if (d_alpha) dpa += d_alpha[bv * P + pid];
-    }
+    PixelSeed sd;
+    pixel_seed<DEPTH, LOSS>(d, inside, bv, P, pid, T_final, bg, cfin, d_img, d_depth, d_alpha, cmask, sd);
+    const float dp0 = sd.dp0, dp1 = sd.dp1, dp2 = sd.dp2, dpd = sd.dpd, dpa = sd.dpa;
+    const float4 cf = sd.cf;
     // per-pixel state entering the chunk: the forward's checkpoint (or the list head)
     float Tr = 1.0f, Dup = 0.f;
     if (slot >= 0) {
@@ -649,6 +775,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const float DK = cdpf - (dpa - bg_dot) * T_final;  // Dfin - K
     float Erem = DK - Dup;  // Dfin - K - D_i, kept directly (one subtraction less per entry)
     const float ddelx_dx = 0.5f * d.W, ddely_dy = 0.5f * d.H;
+    const int det_s = DET ? det_seed_shift(det_max) : 0;
     const size_t gbase = (size_t)bv * d.N;
     // MFMA operands: A (features) lane (ql, qk) holds feature ql of wave pixels 32 t + 8 qk + j, j = 0..7
     const int ql = lane & 15, qk = lane >> 4;
@@ -858,14 +985,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const float Sxy = fmaf(xg, fmaf(yg, q[0], -q[2]), fmaf(-yg, q[1], q[4]));
             const float Syy = fmaf(yg, fmaf(yg, q[0], -2.f * q[2]), q[5]);
             float *o = sAccW[0];
-            o[0 * LS + j] = -ddelx_dx * (cA * Sx + cB * Sy);
-            o[1 * LS + j] = -ddely_dy * (cC * Sy + cB * Sx);
-            o[2 * LS + j] = -0.5f * Sxx;
-            o[3 * LS + j] = -0.5f * Sxy;
-            o[4 * LS + j] = -0.5f * Syy;
-            o[5 * LS + j] = op > 0.f ? q[0] / op : 0.f;
+            float part[NACC];
+            part[0] = -ddelx_dx * (cA * Sx + cB * Sy);
+            part[1] = -ddely_dy * (cC * Sy + cB * Sx);
+            part[2] = -0.5f * Sxx;
+            part[3] = -0.5f * Sxy;
+            part[4] = -0.5f * Syy;
+            part[5] = op > 0.f ? q[0] / op : 0.f;
 #pragma unroll
-            for (int qq = 6; qq < NV; qq++) o[qq * LS + j] = q[qq];
+            for (int qq = 6; qq < NV; qq++) part[qq] = q[qq];
+            if (DET) {  // fixed-point units: the call's seed scale and the record's normalisers (exact powers of two)
+                const DetNorm nm = det_norm(Pj.z, Pj.w, Qj.x, d.W, d.H);
+#pragma unroll
+                for (int qq = 0; qq < NV; qq++) part[qq] = ldexpf(part[qq], det_s + (qq < 5 ? nm.k[qq] : 0));
+            }
+#pragma unroll
+            for (int qq = 0; qq < NV; qq++) o[qq * LS + j] = part[qq];
         }
         vm_wait_all();  // the next chunk's DMA and ids have landed: the atomics below cannot delay them
         __syncthreads();
@@ -880,9 +1015,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
                 const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
                 if (a != 0.f) {
-                    if (DET)  // integer adds commute: order-independent sums
+                    if (DET)  // integer adds commute: order-independent sums (a is already in fixed-point units)
                         atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
-                                  (unsigned long long)__float2ll_rn(a * DET_SCALE));
+                                  (unsigned long long)__float2ll_rn(fminf(fmaxf(a, -9.0e18f), 9.0e18f)));
                     else
                         atomicAdd(accum + ai, a);
                 }
@@ -902,7 +1037,11 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
                                                      const float *__restrict__ views,
                                                      const float *__restrict__ projs, const uint2 *__restrict__ rects,
                                                      float *__restrict__ accum, float *__restrict__ d_gauss,
-                                                     float *__restrict__ d_means2D) {
+                                                     float *__restrict__ d_means2D, const float4 *__restrict__ gP,
+                                                     const float4 *__restrict__ gQ,
+                                                     const unsigned *__restrict__ det_max) {
+    const bool det = (d.options & LGM_RENDER_DETERMINISTIC) != 0;
+    const int det_s = det ? det_seed_shift(det_max) : 0;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
     if (i >= d.N) return;
@@ -927,13 +1066,15 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
             continue;
         }
         float acc[NACC_V];
-        if (d.options & LGM_RENDER_DETERMINISTIC) {
+        if (det) {  // back from fixed point: the same normalisers k_render_bwd derived from this record
             const longlong2 *acc2 = reinterpret_cast<const longlong2 *>(accum) + k * (NACC_V / 2);
+            const float4 rp = gP[k];
+            const DetNorm nm = det_norm(rp.z, rp.w, gQ[k].x, d.W, d.H);
 #pragma unroll
             for (int q = 0; q < NACC_V / 2; q++) {
                 const longlong2 a = acc2[q];
-                acc[2 * q] = (float)((double)a.x * (1.0 / DET_SCALE));
-                acc[2 * q + 1] = (float)((double)a.y * (1.0 / DET_SCALE));
+                acc[2 * q] = (float)ldexp((double)a.x, -(det_s + nm.k[2 * q]));
+                acc[2 * q + 1] = (float)ldexp((double)a.y, -(det_s + nm.k[2 * q + 1]));
             }
         } else {
             const float2 *acc2 = reinterpret_cast<const float2 *>(accum + k * NACC_V);
@@ -1005,11 +1146,11 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
     }
     {  // the scene's view-independent partials (opacity, colour), summed over its views by the backward's atomics
         const size_t ks = (size_t)d.BV * d.N * NACC_V + ((size_t)b * d.N + i) * NACC_S;
-        if (d.options & LGM_RENDER_DETERMINISTIC) {
+        if (det) {
             const long long *a = reinterpret_cast<const long long *>(accum) + ks;
-            dop = (float)((double)a[0] * (1.0 / DET_SCALE));
+            dop = (float)ldexp((double)a[0], -det_s);
 #pragma unroll
-            for (int q = 0; q < 3; q++) dcol[q] = (float)((double)a[1 + q] * (1.0 / DET_SCALE));
+            for (int q = 0; q < 3; q++) dcol[q] = (float)ldexp((double)a[1 + q], -det_s);
         } else {
             const float4 a = *reinterpret_cast<const float4 *>(accum + ks);
             dop = a.x;
@@ -1070,8 +1211,10 @@ int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, fl
 
 int launch_loss_reduce(const Dims &d, char *ws, const Layout &L, hipStream_t st) {
     const double P = (double)d.H * d.W;
-    LGM_LAUNCH("k_loss_reduce", st, (k_loss_reduce<<<1, 256, 0, st>>>(d.BV * d.T, (const float *)(ws + L.lossp),
-                                                                      3.0 * d.BV * P, d.BV * P, d.loss_out)));
+    const int M = d.BV * d.T, G = (M + LR_TILES - 1) / LR_TILES;
+    LGM_LAUNCH("k_loss_reduce", st, (k_loss_reduce<<<G, LR_THREADS, 0, st>>>(
+                                        M, (const float2 *)(ws + L.lossp), 3.0 * d.BV * P, d.BV * P,
+                                        (double2 *)(ws + L.lossw), (unsigned *)(ws + L.misc) + 12, d.loss_out)));
     return LGM_OK;
 }
 
@@ -1087,6 +1230,19 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
         return LGM_E_HIP;
     }
     const bool loss = (d.options & LGM_RENDER_FUSED_LOSS) != 0, det = (d.options & LGM_RENDER_DETERMINISTIC) != 0;
+    unsigned *det_max = (unsigned *)(ws + L.misc) + 13;
+    if (det) {  // the call's fixed-point scale: max |dL/dpixel| over every seed (k_det_seed_max)
+        if (hipMemsetAsync(det_max, 0, 4, st) != hipSuccess) {
+            set_error("hipMemsetAsync failed");
+            return LGM_E_HIP;
+        }
+        auto smax = loss ? (d_depth ? k_det_seed_max<true, true> : k_det_seed_max<false, true>)
+                         : (d_depth ? k_det_seed_max<true, false> : k_det_seed_max<false, false>);
+        LGM_LAUNCH("k_det_seed_max", st, (smax<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
+                                             d, (const float *)(ws + L.final_T), bg, (const float4 *)(ws + L.cfin),
+                                             d_image, d_depth, d_alpha, (const unsigned char *)(ws + L.cmask),
+                                             det_max)));
+    }
     auto pick = [&](auto depth_tag) {
         constexpr bool DP = decltype(depth_tag)::value;
         return loss ? (det ? k_render_bwd<DP, true, true> : k_render_bwd<DP, true, false>)
@@ -1103,14 +1259,15 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
                                        (const int *)(ws + L.wlast), (const float4 *)(ws + L.cfin), (const float *)(ws + L.ck),
                                        (const int2 *)(ws + L.cklist), (const int *)(ws + L.nck),
                                        (const unsigned *)(ws + L.misc) + 4, L.ck_region, d_image, d_depth, d_alpha,
-                                       (const unsigned char *)(ws + L.cmask), (float *)(ws + L.accum),
+                                       (const unsigned char *)(ws + L.cmask), (float *)(ws + L.accum), det_max,
                                        // (debug counters: after the per-tile and per-binning-workgroup records)
                                        8 + 8LL * d.BV * d.T + 8LL * d.BV * ((d.N + 511) / 512))));
     dim3 grid((d.N + 255) / 256, d.B);
     LGM_LAUNCH("k_preproc_bwd", st, (k_preproc_bwd<<<grid, 256, 0, st>>>(d, gaussians, cam_view, cam_view_proj,
                                                                         (const uint2 *)(ws + L.rects),
                                                                         (float *)(ws + L.accum), d_gaussians,
-                                                                        d_means2D)));
+                                                                        d_means2D, (const float4 *)(ws + L.gP),
+                                                                        (const float4 *)(ws + L.gQ), det_max)));
     return LGM_OK;
 }
 

@@ -121,15 +121,18 @@ def allreduce_scene_grads(grad, info: RankInfo):
     return grad
 
 
-def make_ddp(module, device=None, bucket_cap_mb: float = 100.0, bf16_compress: bool = True, **kw):
-    """DistributedDataParallel for LGM's training step (main.py:82-109 trains through accelerate's DDP), tuned for
-    one node of MI355X over xGMI: RCCL's ring all-reduce is bound by the 7 point-to-point links
-    (~153 GB/s each), not by launch count, so buckets are larger than DDP's 25 MB default (the 'big' UNet's 1.66 GB
-    of fp32 gradients in ~17 buckets of 100 MB, each still overlapping the backward of the layers before it), and
-    gradients travel as bf16 (torch's bf16_compress_hook: half the link bytes; the optimizer still sees fp32,
-    divided by the world size). Single-process runs return the module unchanged."""
+def make_ddp(module, device=None, bucket_cap_mb: float = 100.0, bf16_compress: bool = False, **kw):
+    """DistributedDataParallel for LGM's training step (main.py:82-109 trains through accelerate's DDP), for one
+    node of MI355X over xGMI: RCCL's ring all-reduce is bound by the 7 point-to-point links
+    (~153 GB/s each), not by launch count, so the default buckets are larger than DDP's 25 MB (the 'big' UNet's
+    1.66 GB of fp32 gradients in ~17 buckets of 100 MB, each still overlapping the backward of the layers before
+    it). Gradients are all-reduced in fp32, as the reference's accelerate DDP does; bf16_compress=True opts into
+    torch's bf16_compress_hook (half the link bytes, gradients rounded to bf16 on the wire -- a numerics change, off
+    by default). The bucket size and the hook are link-bytes arguments, unmeasured on 8 GPUs here (the driver's
+    8-GPU run is the measurement). Wraps whenever a process group is initialised (a one-rank group too: DDP's
+    reducer and hooks then run on the real communicator); without one the module is returned unchanged."""
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return module
     from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
     from torch.nn.parallel import DistributedDataParallel as DDP
@@ -142,9 +145,10 @@ def make_ddp(module, device=None, bucket_cap_mb: float = 100.0, bf16_compress: b
     return ddp
 
 
-def allreduce_bucketed(flat, bucket_elems: int, info: RankInfo, bf16: bool = True):
+def allreduce_bucketed(flat, bucket_elems: int, info: RankInfo, bf16: bool = False):
     """All-reduce (average) of one flat fp32 gradient buffer in buckets, as DDP does at the end of the backward:
-    the communication cost of the training step's parameter gradients (bench.py's cfg5 object)."""
+    the communication cost of the training step's parameter gradients (bench.py's cfg5 object). fp32 on the wire
+    by default (the reference's numerics); bf16=True halves the bytes (make_ddp's bf16_compress)."""
     if info.world <= 1:
         return flat
     import torch

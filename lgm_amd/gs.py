@@ -17,21 +17,27 @@ import torch
 from . import _native
 from .ply import read_ply, write_ply
 
-# Slot-mode (sync-free, worst-case B*V*T*N pair slots) workspace when it fits this many bytes; otherwise the pairs
-# are counted exactly first (one host sync per batch -- the reference syncs once per VIEW for num_rendered).
-# Default: a quarter of the device's HBM (72 GB of an MI355X's 288: cfg3 needs 1.2 GB, the 8-scene pool 9.8 GB,
-# LGM 'big' with 20 views at 512^2 25 GB). LGM_AMD_WS_BUDGET_GB overrides.
+# Slot-mode (sync-free, worst-case B*V*T*N pair slots) workspace when it fits; otherwise the pairs are counted
+# exactly first (one host sync per batch -- the reference syncs once per VIEW for num_rendered). The slot workspace
+# costs address space, not traffic (only the used part of each tile bucket is touched), but it is held from the
+# forward to the backward: up to _WS_FREE_SLOT bytes it is taken without asking (cfg3 needs 1.2 GB, the 8-scene
+# pool 9.8 GB); above, only if it fits half of the memory torch could still hand out (free device memory plus
+# torch's cached-but-unused blocks) -- LGM 'big' with 20 views at 512^2 needs 25 GB, a 64-view training batch at
+# 512^2 34 GB: taken on an idle 288 GB MI355X, counted exactly next to a large model. LGM_AMD_WS_BUDGET_GB fixes
+# the limit instead.
 _WS_BUDGET = int(float(os.environ["LGM_AMD_WS_BUDGET_GB"]) * (1 << 30)) if "LGM_AMD_WS_BUDGET_GB" in os.environ \
     else None
-_dev_mem = {}
+_WS_FREE_SLOT = 16 << 30
 
 
-def _ws_budget(dev) -> int:
+def _slot_fits(ws_bytes: int, dev) -> bool:
     if _WS_BUDGET is not None:
-        return _WS_BUDGET
-    if dev not in _dev_mem:
-        _dev_mem[dev] = torch.cuda.get_device_properties(dev).total_memory
-    return _dev_mem[dev] // 4
+        return ws_bytes <= _WS_BUDGET
+    if ws_bytes <= _WS_FREE_SLOT:
+        return True
+    free, _ = torch.cuda.mem_get_info(dev)
+    avail = free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    return ws_bytes <= avail // 2
 
 
 def _tiles(H: int, W: int) -> int:
@@ -51,7 +57,7 @@ class _RasterizeBatched(torch.autograd.Function):
         stream = _native.stream_of(dev)
         cap = 0
         ws_bytes = L.lgm_render_workspace_size_opts(B, V, N, H, W, 0, options)
-        if ws_bytes > _ws_budget(dev):
+        if not _slot_fits(ws_bytes, dev):
             # exact pair count (the reference syncs once per view for this; we sync once per batch)
             small = L.lgm_render_workspace_size(B, V, N, H, W, 1)
             ws = torch.empty(small, dtype=torch.uint8, device=dev)
@@ -112,7 +118,10 @@ class _RasterizeBatched(torch.autograd.Function):
                 raise NotImplementedError("a depth gradient together with the fused loss (LGM's loss has no depth)")
             # d/dmse_image of loss_mse, mse_image and psnr = -10 log10(mse_image); d/dmse_alpha of loss_mse, mse_alpha
             d4 = d_loss4.float()
-            s2 = torch.stack([d4[0] + d4[1] - d4[3] * (10.0 / math.log(10.0)) / loss4[1], d4[0] + d4[2]]).contiguous()
+            # the PSNR term only where psnr is actually differentiated (GaussianRenderer.render detaches it, as the
+            # reference computes it under no_grad): an exact fit (mse_image == 0) must not turn 0 / 0 into NaN
+            d_psnr = torch.where(d4[3] != 0, d4[3] * (10.0 / math.log(10.0)) / loss4[1], torch.zeros_like(d4[3]))
+            s2 = torch.stack([d4[0] + d4[1] - d_psnr, d4[0] + d4[2]]).contiguous()
             _native.check(L.lgm_render_backward_loss(B, V, N, H, W, _native.ptr(g), _native.ptr(cam_view),
                                                      _native.ptr(cam_view_proj), _native.ptr(bg), tanx, tany,
                                                      scale_modifier, _native.ptr(d_image), _native.ptr(d_alpha),

@@ -28,3 +28,17 @@ def cuda():
     from lgm_amd import build as B
     B.build()
     return torch.device("cuda:0")
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Write the gradient-precision records of this session's GPU parity tests (tests/render_cases.PRECISION)."""
+    try:
+        from tests.render_cases import PRECISION
+    except Exception:
+        return
+    if PRECISION:
+        import json
+        out = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "grad_precision.json"), "w") as f:
+            json.dump(PRECISION, f, indent=1)

@@ -8,6 +8,9 @@ from lgm_amd.cameras import orbit_cameras, tan_half_fov
 from lgm_amd.synthetic import synthetic_gaussians
 
 TAN = tan_half_fov(49.1)
+# gradient-precision records (bar and measured errors per parameter group) the GPU parity tests append; the session
+# writes them to gpurun_out/grad_precision.json (tests/conftest.py)
+PRECISION = []
 
 
 def scene(B=1, N=1000, V=2, seed=0, shrink=1.0, scale_mul=1.0, elevation=0.0, az_offset=0.0, max_opacity=None):

@@ -233,3 +233,31 @@ def test_attention_deterministic(cuda):
         o.backward(d_o)
         outs.append((o, x.grad))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("where", ["q", "k", "v"])
+def test_nan_propagates_like_sdpa(cuda, dtype, where):
+    """A NaN anywhere in q/k/v reaches the output and the gradients exactly where torch's attention puts it (the
+    divergence detection of a bf16 training run relies on NaN propagation; attention.hip is built without IEEE NaN
+    semantics for its max / exp chains, so this pins that no NaN is dropped): NaN masks of o and of dqkv equal
+    those of the fp32 torch math on the same inputs."""
+    from lgm_amd.attention import packed_attention
+    B, L, H, D = 2, 200, 2, 32
+    gen = torch.Generator().manual_seed(9)
+    qkv = torch.randn(B, L, 3, H, D, generator=gen)
+    qkv[1, 37, "qkv".index(where), 1, 5] = float("nan")
+    d_o = torch.randn(B, L, H, D, generator=gen)
+    x = qkv.to(cuda, dtype).requires_grad_(True)
+    o = packed_attention(x)
+    o.backward(d_o.to(cuda, dtype))
+    torch.cuda.synchronize()
+    xr = qkv.clone().requires_grad_(True)
+    q, k, v = (xr[:, :, i].transpose(1, 2) for i in range(3))
+    p = torch.softmax((q * D ** -0.5) @ k.transpose(-1, -2), dim=-1)
+    orf = (p @ v).transpose(1, 2)
+    orf.backward(d_o)
+    assert torch.isnan(orf).any()
+    assert torch.equal(torch.isnan(o.float().cpu()), torch.isnan(orf)), "output NaN pattern differs"
+    assert torch.equal(torch.isnan(x.grad.float().cpu()), torch.isnan(xr.grad)), "gradient NaN pattern differs"

@@ -1,0 +1,66 @@
+"""SURVEY §8(f)3 on the GPU: infer.py:114-145's 180-frame orbit video as batched renders with device-side cameras
+(lgm_amd.cameras.render_orbit_frames) against the reference's per-frame loop restated line by line (numpy
+orbit_camera -> flip -> torch.inverse -> transpose -> @ proj -> render(V = 1) -> (image * 255).astype(uint8)) on
+the same HIP renderer. The two camera constructions differ in the last float bits (closed-form rigid inverse vs
+torch.inverse), so the uint8 frames are compared with a pixel budget instead of bit for bit."""
+import numpy as np
+import pytest
+import torch
+
+from lgm_amd import GaussianRenderer, Options
+from lgm_amd.cameras import orbit_camera, orbit_cameras_batched, projection_matrix, render_orbit_frames
+from lgm_amd.synthetic import synthetic_gaussians
+
+pytestmark = pytest.mark.gpu
+
+
+def _reference_loop(renderer, gaussians, azimuths, scales, radius, dev):
+    """infer.py:132-145 (and :116-131 with per-frame scale_modifier), one render per azimuth."""
+    opt = renderer.opt
+    proj = projection_matrix(opt.fovy, opt.znear, opt.zfar).to(dev)
+    images = []
+    for azi, sc in zip(azimuths, scales):
+        cam_poses = torch.from_numpy(orbit_camera(0, azi, radius=radius, opengl=True)).unsqueeze(0).to(dev)
+        cam_poses[:, :3, 1:3] *= -1
+        cam_view = torch.inverse(cam_poses).transpose(1, 2)
+        cam_view_proj = cam_view @ proj
+        cam_pos = -cam_poses[:, :3, 3]
+        image = renderer.render(gaussians, cam_view.unsqueeze(0), cam_view_proj.unsqueeze(0), cam_pos.unsqueeze(0),
+                                scale_modifier=sc)["image"]
+        images.append((image.squeeze(1).permute(0, 2, 3, 1).contiguous().float().cpu().numpy() * 255)
+                      .astype(np.uint8))
+    return np.concatenate(images, axis=0)
+
+
+@pytest.mark.parametrize("fancy", [False, True])
+def test_orbit_video_batched_matches_per_frame_loop(cuda, fancy):
+    renderer = GaussianRenderer(Options(output_size=256))
+    g = synthetic_gaussians(1, 30_000, seed=12).to(cuda)
+    if fancy:  # infer.py:116-131: azimuths 0..716 step 4, scale_modifier min(azi / 360, 1)
+        az = np.arange(0, 720, 4, dtype=np.int32)
+        scales = [min(a / 360, 1) for a in az]
+    else:  # infer.py:134-145: azimuths 0..358 step 2
+        az = np.arange(0, 360, 2, dtype=np.int32)
+        scales = [1] * len(az)
+    ref = _reference_loop(renderer, g, az, scales, 1.5, cuda)
+    got = render_orbit_frames(renderer, g, torch.from_numpy(az.astype(np.float32)), radius=1.5,
+                              scale_modifier=np.asarray(scales, dtype=np.float64)).cpu().numpy()
+    assert got.shape == ref.shape == (len(az), 256, 256, 3)
+    diff = np.abs(got.astype(np.int32) - ref.astype(np.int32))
+    frac = float((diff > 0).mean())
+    print(f"fancy={fancy}: {frac:.2e} of the frame pixels differ, max {diff.max()}")
+    assert frac < 1e-3 and diff.max() <= 2, (frac, int(diff.max()))
+
+
+def test_device_cameras_match_reference_recipe(cuda):
+    """orbit_cameras_batched (device, closed form) vs the per-frame recipe's matrices."""
+    az = np.arange(0, 360, 2, dtype=np.float32)
+    cv, cvp, cp = orbit_cameras_batched(0.0, torch.from_numpy(az), 1.5, device=cuda)
+    proj = projection_matrix(49.1, 0.5, 2.5)
+    for i in (0, 17, 45, 90, 179):
+        pose = torch.from_numpy(orbit_camera(0, float(az[i]), radius=1.5, opengl=True)).unsqueeze(0)
+        pose[:, :3, 1:3] *= -1
+        v = torch.inverse(pose.double()).transpose(1, 2)
+        torch.testing.assert_close(cv[i].double().cpu(), v[0], rtol=0, atol=1e-6)
+        torch.testing.assert_close(cvp[i].double().cpu(), (v @ proj.double())[0], rtol=0, atol=2e-6)
+        torch.testing.assert_close(cp[i].double().cpu(), -pose[0, :3, 3].double(), rtol=0, atol=1e-6)

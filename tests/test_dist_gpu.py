@@ -103,3 +103,108 @@ def test_rccl_collectives_single_rank(cuda, tmp_path):
     np.testing.assert_array_equal(z["summed"], z["grad"])
     np.testing.assert_allclose(z["red"], z["flat"] / 2, rtol=0, atol=0)
     assert float(z["mx"]) == 3.5
+
+
+class _TinyLGM(torch.nn.Module):
+    """A stand-in for LGM's trainable part: a conv for the UNet (9 -> 14 channels, as core/unet.py's in/out) and
+    the fused Gaussian head (core/models.py:96-117) -- enough to exercise DDP's reducer on real gradients of the
+    render path."""
+
+    def __init__(self):
+        super().__init__()
+        from lgm_amd.head import GaussianHead
+        self.unet = torch.nn.Conv2d(9, 14, 3, padding=1)
+        self.head = GaussianHead()
+        with torch.no_grad():  # splats of the synthetic distribution's size (as bench.cfg5_inputs)
+            self.head.conv.weight.copy_(torch.diag(torch.tensor([0.35] * 3 + [1.0] * 11)).view(14, 14, 1, 1))
+            self.head.conv.bias.zero_()
+            self.head.conv.bias[4:7] = -2.2522
+
+    def forward(self, images):  # [V_in, 9, h, w] -> gaussians [1, V_in*h*w, 14]
+        return self.head(self.unet(images), 1, images.shape[0])
+
+
+def _train_step(model, opt, images, cams, gt, mask, bg, renderer):
+    """main.py:99-109: forward, render + fused MSE loss (core/models.py:141-148), backward, clip, AdamW step."""
+    opt.zero_grad()
+    g = model(images)
+    out = renderer.render(g, *cams, bg_color=bg, gt_images=gt, gt_masks=mask)
+    out["loss_mse"].backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+    grads = [p.grad.detach().clone() for p in model.parameters()]
+    opt.step()
+    return float(out["loss_mse"]), grads
+
+
+def _ddp_inputs(dev):
+    from lgm_amd import GaussianRenderer, Options
+    from lgm_amd.cameras import orbit_cameras
+    gen = torch.Generator().manual_seed(31)
+    images = torch.randn(4, 9, 32, 32, generator=gen).to(dev)
+    cams = tuple(t[None].to(dev) for t in orbit_cameras(4, elevation=-10.0))
+    gt = torch.rand(1, 4, 3, 96, 96, generator=gen).to(dev)
+    mask = (torch.rand(1, 4, 1, 96, 96, generator=gen) > 0.5).float().to(dev)
+    bg = torch.rand(3, generator=gen).to(dev)
+    return images, cams, gt, mask, bg, GaussianRenderer(Options(output_size=96))
+
+
+def _ddp_worker(tmp, bf16):
+    """make_ddp on a real RCCL communicator (one rank on cuda:0): two training steps through DDP's reducer
+    (100 MB buckets; fp32 or the bf16 compression hook), deterministic render gradients."""
+    import torch.distributed as dist
+    os.environ["LGM_AMD_DETERMINISTIC"] = "1"
+    torch.backends.cudnn.deterministic = True
+    info = D.rank_info()
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=info.rank, world_size=info.world, device_id=dev)
+    try:
+        torch.manual_seed(3)
+        model = _TinyLGM().to(dev)
+        ddp = D.make_ddp(model, device=dev, bf16_compress=bf16)
+        assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel)
+        opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3)
+        inputs = _ddp_inputs(dev)
+        losses, grads = [], []
+        for _ in range(2):
+            l, gr = _train_step(ddp, opt, *inputs)
+            losses.append(l)
+            grads.append(gr)
+        torch.cuda.synchronize()
+        np.savez(os.path.join(tmp, "ddp.npz"), losses=np.array(losses),
+                 **{f"g{s}_{i}": t.cpu().numpy() for s, gr in enumerate(grads) for i, t in enumerate(gr)},
+                 **{f"p_{i}": p.detach().cpu().numpy() for i, p in enumerate(model.parameters())},
+                 backend=np.array(dist.get_backend()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_make_ddp_rccl_single_rank(cuda, tmp_path, monkeypatch, bf16):
+    """The DDP-wrapped training step on RCCL equals the same step without DDP: to fp32 rounding with fp32 gradients
+    (a one-rank all-reduce averages by 1; the render and head gradients are deterministic, the stand-in conv's
+    MIOpen backward need not be bitwise across processes), to bf16 rounding with the compression hook; the
+    parameters after AdamW likewise."""
+    D.spawn_ranks(_ddp_worker, 1, str(tmp_path), bf16)
+    z = np.load(os.path.join(tmp_path, "ddp.npz"))
+    assert str(z["backend"]) == "nccl"
+    monkeypatch.setenv("LGM_AMD_DETERMINISTIC", "1")
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    torch.manual_seed(3)
+    model = _TinyLGM().to(cuda)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    inputs = _ddp_inputs(cuda)
+    for s in range(2):
+        loss, grads = _train_step(model, opt, *inputs)
+        for i, gr in enumerate(grads):
+            got = z[f"g{s}_{i}"]
+            if bf16:
+                err = np.abs(got - gr.cpu().numpy()).max()
+                assert err <= 2.0 ** -7 * np.abs(gr.cpu().numpy()).max() + 1e-12, (s, i, err)
+            else:
+                ref = gr.cpu().numpy()
+                np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+        assert abs(float(z["losses"][s]) - loss) <= 1e-6 * abs(loss)
+    for i, p in enumerate(model.parameters()):
+        ref = p.detach().cpu().numpy()
+        np.testing.assert_allclose(z[f"p_{i}"], ref, rtol=0, atol=(1e-3 if bf16 else 1e-6) * np.abs(ref).max())

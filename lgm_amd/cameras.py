@@ -140,15 +140,19 @@ def orbit_cameras_batched(elevation, azimuth, radius: float = 1.5, fovy: float =
 
 
 def render_orbit_frames(renderer, gaussians, azimuths, elevation: float = 0.0, radius: float = 1.5,
-                        scale_modifier=1.0, chunk: int = 60):
+                        scale_modifier=1.0, chunk: int = 60, cameras=None):
     """infer.py:114-145's video loops (one render per azimuth) as batched renders of up to `chunk` views each, with
     the cameras built on the device: returns uint8 frames [V, H, W, 3] (on the renderer's device), each
     (image * 255) truncated as the reference's .astype(np.uint8). scale_modifier: one float, or one per azimuth
     (infer.py's fancy_video renders azimuth a with min(a / 360, 1), :129-131); consecutive frames with the same
-    scale share a call."""
+    scale share a call. cameras: (cam_view [V,4,4], cam_view_proj [V,4,4], cam_pos [V,3]) to use instead of the
+    device-built orbit."""
     opt = renderer.opt
     dev = gaussians.device
-    cv, cvp, cp = orbit_cameras_batched(elevation, azimuths, radius, opt.fovy, opt.znear, opt.zfar, device=dev)
+    if cameras is None:
+        cv, cvp, cp = orbit_cameras_batched(elevation, azimuths, radius, opt.fovy, opt.znear, opt.zfar, device=dev)
+    else:
+        cv, cvp, cp = (t.to(dev) for t in cameras)
     V = cv.shape[0]
     sm = np.broadcast_to(np.asarray(scale_modifier, dtype=np.float64), (V,))
     frames = []

@@ -90,6 +90,9 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #ifndef LGM_BWD_EARLY_STAGE
 #define LGM_BWD_EARLY_STAGE 1  // the first chunk's staging goes out before the per-pixel state loads (bwd 647 -> 644 us)
 #endif
+#ifndef LGM_BWD_PIPE
+#define LGM_BWD_PIPE 1  // software-pipelined moment flush (k_render_bwd): batch k's MFMAs overlap batch k + 1's evaluation
+#endif
 #ifndef LGM_BWD_CHUNK
 #define LGM_BWD_CHUNK 64  // backward entries per staged chunk (the per-wave moment slots scale with it)
 #endif
@@ -618,8 +621,10 @@ __device__ __forceinline__ DetNorm det_norm(float Ap, float Bp, float Cp, int W,
     return n;
 }
 
-// k_det_seed_max: grid (B*V*T), block 256: max |dL/dpixel| over every seed of the call -> *det_max (float bits,
-// atomicMax on the non-negative bit pattern; zeroed by the caller).
+// k_det_seed_max: grid (min(B*V*T, DET_MAX_WGS)), block 256, each workgroup striding over tiles: max |dL/dpixel|
+// over every seed of the call -> *det_max (float bits, atomicMax on the non-negative bit pattern; zeroed by the
+// caller). One atomic per workgroup: same-address atomics serialise (one per wave over 12,288 tiles took 564 us).
+constexpr int DET_MAX_WGS = 512;
 template <bool DEPTH, bool LOSS>
 __global__ __launch_bounds__(256) void k_det_seed_max(Dims d, const float *__restrict__ final_T,
                                                       const float *__restrict__ bg, const float4 *__restrict__ cfin,
@@ -627,23 +632,31 @@ __global__ __launch_bounds__(256) void k_det_seed_max(Dims d, const float *__res
                                                       const float *__restrict__ d_alpha,
                                                       const unsigned char *__restrict__ cmask,
                                                       unsigned *__restrict__ det_max) {
-    const int tile = blockIdx.x;
-    const int bv = tile / d.T, t = tile - bv * d.T;
-    const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
+    __shared__ unsigned s_m[4];
     int lx, ly;
     tile_pixel(threadIdx.x, lx, ly);
-    const int px = tx0 + lx, py = ty0 + ly;
-    const bool inside = px < d.W && py < d.H;
     const size_t P = (size_t)d.H * d.W;
-    const size_t pid = inside ? (size_t)d.W * py + px : 0;
-    PixelSeed sd;
-    pixel_seed<DEPTH, LOSS>(d, inside, bv, P, pid, inside ? final_T[bv * P + pid] : 0.f, bg, cfin, d_img, d_depth,
-                            d_alpha, cmask, sd);
-    float m = fmaxf(fmaxf(fabsf(sd.dp0), fabsf(sd.dp1)), fmaxf(fmaxf(fabsf(sd.dp2), fabsf(sd.dpd)), fabsf(sd.dpa)));
+    float m = 0.f;
+    for (int tile = blockIdx.x; tile < d.BV * d.T; tile += gridDim.x) {
+        const int bv = tile / d.T, t = tile - bv * d.T;
+        const int px = (t % d.gx) * BX + lx, py = (t / d.gx) * BY + ly;
+        const bool inside = px < d.W && py < d.H;
+        const size_t pid = inside ? (size_t)d.W * py + px : 0;
+        PixelSeed sd;
+        pixel_seed<DEPTH, LOSS>(d, inside, bv, P, pid, inside ? final_T[bv * P + pid] : 0.f, bg, cfin, d_img, d_depth,
+                                d_alpha, cmask, sd);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(sd.dp0), fabsf(sd.dp1)),
+                           fmaxf(fmaxf(fabsf(sd.dp2), fabsf(sd.dpd)), fabsf(sd.dpa))));
+    }
     unsigned mb = __float_as_uint(m);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o, 64));
-    if ((threadIdx.x & 63) == 0 && mb) atomicMax(det_max, mb);
+    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = mb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        mb = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+        if (mb) atomicMax(det_max, mb);
+    }
 }
 
 // k_render_bwd: grid (B*V*T + CK slots), block 256. DEPTH: an upstream depth gradient is present (LGM passes none).
@@ -826,21 +839,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     int myj = 0;  // the chunk row of this lane's batch column (ql & 7)
-    auto flush_batch = [&]() {
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        // B operand: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t), split hi + lo
-        f32x4 a2[2];
+    // B operand of the current batch: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t)
+    auto read_batch = [&](float (&xs)[2][8]) {
 #pragma unroll
         for (int t2 = 0; t2 < 2; t2++) {
             const float4 *src = reinterpret_cast<const float4 *>(myWU + ql * WU_LD + 32 * t2 + 8 * qk);
             const float4 x0 = src[0], x1 = src[1];
-            const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            xs[t2][0] = x0.x; xs[t2][1] = x0.y; xs[t2][2] = x0.z; xs[t2][3] = x0.w;
+            xs[t2][4] = x1.x; xs[t2][5] = x1.y; xs[t2][6] = x1.z; xs[t2][7] = x1.w;
+        }
+    };
+    // split hi + lo, the moment MFMAs, and the lane's (at most 4) live results into this wave's slots
+    auto mfma_batch = [&](const float (&xs)[2][8], int col) {
+        f32x4 a2[2];
+#pragma unroll
+        for (int t2 = 0; t2 < 2; t2++) {
             bf16x8 bh, bl;
 #pragma unroll
             for (int j = 0; j < 8; j++) {  // hi = the top 16 bits (exact), lo = the rest rounded: ~2^-17 relative
-                const unsigned ub = __builtin_bit_cast(unsigned, xs[j]);
+                const unsigned ub = __builtin_bit_cast(unsigned, xs[t2][j]);
                 bh[j] = __builtin_bit_cast(__bf16, (unsigned short)(ub >> 16));
-                bl[j] = (__bf16)(xs[j] - __builtin_bit_cast(float, ub & 0xffff0000u));
+                bl[j] = (__bf16)(xs[t2][j] - __builtin_bit_cast(float, ub & 0xffff0000u));
             }
             f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);
@@ -851,9 +870,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         // D[row = 4 qk + r][col = ql]: moments 0..5 in the w columns, rows 6..9 in the u columns; each lane stores its
         // (at most 4) live results into this wave's slots at a per-lane row offset fixed for the kernel (mrow)
 #pragma unroll
-        for (int rr = 0; rr < 4; rr++) myAcc[mrow[rr] + myj] = acc[rr];  // (sentinel columns: row CH, all zero)
+        for (int rr = 0; rr < 4; rr++) myAcc[mrow[rr] + col] = acc[rr];  // (sentinel columns: row CH, all zero)
+    };
+#if !LGM_BWD_PIPE
+    auto flush_batch = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        float xs[2][8];
+        read_batch(xs);
+        mfma_batch(xs, myj);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     };
+#endif
 
     // Staging pipeline (front to back over [s0, s1)): chunk b0 + CH streams into the other buffer by LDS DMA
     // during chunk b0's compositing and is complete (vm_wait_all) before chunk b0's gradient atomics are issued,
@@ -914,7 +941,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         const int lastrel = last - b0;  // this pixel's last contributor, relative to the chunk
         uint2 lraw[2];  // the next step's list words, read one step ahead
         list_raw<MB>(S, w, 0, lraw);
-        for (int kk = 0; kk < cnt; kk += MB) {
+        // one batch: MB list entries evaluated per pixel, their w and u written to this wave's WU image
+        auto eval_batch = [&](int kk) {
             int jj8[MB];
             list_decode<MB>(lraw, jj8);
             myj = S.list[w][kk + (lane & (MB - 1))];  // the entry of this lane's batch column
@@ -959,8 +987,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                     myWU[(MB + 4 * h + u) * WU_LD + lane] = aT;            // u (dchannel_dcolor)
                 }
             }
+        };
+#if LGM_BWD_PIPE
+        // software-pipelined: batch k's B operand is read from the WU image BEFORE batch k + 1 overwrites it (a
+        // wave's LDS operations complete in issue order), so batch k's LDS round trip and moment MFMAs overlap batch
+        // k + 1's evaluations instead of stalling the wave between batches
+        if (cnt > 0) {
+            eval_batch(0);
+            for (int kk = 0; kk < cnt; kk += MB) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                float xs[2][8];
+                read_batch(xs);
+                const int col = myj;
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // (the reads issue before the next writes)
+                if (kk + MB < cnt) eval_batch(kk + MB);
+                mfma_batch(xs, col);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        }
+#else
+        for (int kk = 0; kk < cnt; kk += MB) {
+            eval_batch(kk);
             flush_batch();
         }
+#endif
         __syncthreads();
         // moments -> gradient partials (one thread per staged entry): the sum over the four waves' slots,
         // converted, into wave 0's slots
@@ -1238,7 +1288,7 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
         }
         auto smax = loss ? (d_depth ? k_det_seed_max<true, true> : k_det_seed_max<false, true>)
                          : (d_depth ? k_det_seed_max<true, false> : k_det_seed_max<false, false>);
-        LGM_LAUNCH("k_det_seed_max", st, (smax<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
+        LGM_LAUNCH("k_det_seed_max", st, (smax<<<(unsigned)min(d.BV * d.T, DET_MAX_WGS), 256, 0, st>>>(
                                              d, (const float *)(ws + L.final_T), bg, (const float4 *)(ws + L.cfin),
                                              d_image, d_depth, d_alpha, (const unsigned char *)(ws + L.cmask),
                                              det_max)));

@@ -1,8 +1,8 @@
 """SURVEY §8(f)3 on the GPU: infer.py:114-145's 180-frame orbit video as batched renders with device-side cameras
 (lgm_amd.cameras.render_orbit_frames) against the reference's per-frame loop restated line by line (numpy
 orbit_camera -> flip -> torch.inverse -> transpose -> @ proj -> render(V = 1) -> (image * 255).astype(uint8)) on
-the same HIP renderer. The two camera constructions differ in the last float bits (closed-form rigid inverse vs
-torch.inverse), so the uint8 frames are compared with a pixel budget instead of bit for bit."""
+the same HIP renderer: bit for bit on the loop's own camera matrices; with the device-built cameras (closed-form
+rigid inverse vs torch.inverse: last-bit differences) within a pixel budget."""
 import numpy as np
 import pytest
 import torch
@@ -14,17 +14,23 @@ from lgm_amd.synthetic import synthetic_gaussians
 pytestmark = pytest.mark.gpu
 
 
-def _reference_loop(renderer, gaussians, azimuths, scales, radius, dev):
-    """infer.py:132-145 (and :116-131 with per-frame scale_modifier), one render per azimuth."""
+def _reference_cameras(renderer, azimuths, radius, dev):
+    """infer.py:119-125 per frame: numpy orbit_camera -> flip -> torch.inverse -> transpose -> @ proj."""
     opt = renderer.opt
     proj = projection_matrix(opt.fovy, opt.znear, opt.zfar).to(dev)
-    images = []
-    for azi, sc in zip(azimuths, scales):
+    cams = []
+    for azi in azimuths:
         cam_poses = torch.from_numpy(orbit_camera(0, azi, radius=radius, opengl=True)).unsqueeze(0).to(dev)
         cam_poses[:, :3, 1:3] *= -1
         cam_view = torch.inverse(cam_poses).transpose(1, 2)
-        cam_view_proj = cam_view @ proj
-        cam_pos = -cam_poses[:, :3, 3]
+        cams.append((cam_view, cam_view @ proj, -cam_poses[:, :3, 3]))
+    return cams
+
+
+def _reference_loop(renderer, gaussians, cams, scales):
+    """infer.py:114-145: one render per azimuth, (image * 255).astype(uint8)."""
+    images = []
+    for (cam_view, cam_view_proj, cam_pos), sc in zip(cams, scales):
         image = renderer.render(gaussians, cam_view.unsqueeze(0), cam_view_proj.unsqueeze(0), cam_pos.unsqueeze(0),
                                 scale_modifier=sc)["image"]
         images.append((image.squeeze(1).permute(0, 2, 3, 1).contiguous().float().cpu().numpy() * 255)
@@ -34,6 +40,9 @@ def _reference_loop(renderer, gaussians, azimuths, scales, radius, dev):
 
 @pytest.mark.parametrize("fancy", [False, True])
 def test_orbit_video_batched_matches_per_frame_loop(cuda, fancy):
+    """Batched (up to 60 views a call) == the per-frame loop bit for bit on the loop's own cameras; with the
+    device-built cameras (last-bit differences in the matrices) the frames agree up to the renderer's
+    discontinuities (a 1/255 alpha threshold or a tile rect edge crossed by a rounding): a pixel budget."""
     renderer = GaussianRenderer(Options(output_size=256))
     g = synthetic_gaussians(1, 30_000, seed=12).to(cuda)
     if fancy:  # infer.py:116-131: azimuths 0..716 step 4, scale_modifier min(azi / 360, 1)
@@ -42,14 +51,21 @@ def test_orbit_video_batched_matches_per_frame_loop(cuda, fancy):
     else:  # infer.py:134-145: azimuths 0..358 step 2
         az = np.arange(0, 360, 2, dtype=np.int32)
         scales = [1] * len(az)
-    ref = _reference_loop(renderer, g, az, scales, 1.5, cuda)
+    cams = _reference_cameras(renderer, az, 1.5, cuda)
+    ref = _reference_loop(renderer, g, cams, scales)
+    stacked = tuple(torch.cat([c[i] for c in cams], 0) for i in range(3))
+    sm = np.asarray(scales, dtype=np.float64)
+    same_cams = render_orbit_frames(renderer, g, torch.from_numpy(az.astype(np.float32)), radius=1.5,
+                                    scale_modifier=sm, cameras=stacked).cpu().numpy()
+    assert same_cams.shape == ref.shape == (len(az), 256, 256, 3)
+    np.testing.assert_array_equal(same_cams, ref)
     got = render_orbit_frames(renderer, g, torch.from_numpy(az.astype(np.float32)), radius=1.5,
-                              scale_modifier=np.asarray(scales, dtype=np.float64)).cpu().numpy()
-    assert got.shape == ref.shape == (len(az), 256, 256, 3)
+                              scale_modifier=sm).cpu().numpy()
     diff = np.abs(got.astype(np.int32) - ref.astype(np.int32))
     frac = float((diff > 0).mean())
-    print(f"fancy={fancy}: {frac:.2e} of the frame pixels differ, max {diff.max()}")
-    assert frac < 1e-3 and diff.max() <= 2, (frac, int(diff.max()))
+    print(f"fancy={fancy}: device cameras: {frac:.2e} of the frame pixels differ, max {diff.max()}, "
+          f"mean {diff.mean():.2e}")
+    assert frac < 1e-3 and diff.mean() < 1e-3, (frac, int(diff.max()))
 
 
 def test_device_cameras_match_reference_recipe(cuda):

@@ -35,7 +35,7 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 //   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
 struct Layout {
     size_t gP, gQ, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, wlast, cfin, ck, cklist, nck, cmask,
-        accum, lossp, lossw, misc, total;
+        accum, lossp, lossw, detmax, misc, total;
     long long cap;
     int ck_region;  // backward checkpoint slots per region (8 regions; the forward shards tiles over them)
     bool slot;
@@ -57,7 +57,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.tile_count = take(BV * T * 4);
     L.misc = take(64);  // right after tile_count: the binning clears both with one memset (u64 [0..1]: pair
                         // counts of k_bin; u32 [4..11]: the backward-checkpoint region counters; u32 [12]: the
-                        // fused loss reduction's arrival counter; u32 [13]: deterministic mode's max |dL/dpixel|)
+                        // fused loss reduction's arrival counter)
     L.tile_start = take((BV * T + 1) * 4);
     L.order = take(BV * T * 4);
     L.pairs = take((size_t)L.cap * 8);
@@ -74,6 +74,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.accum = take(acc_elems(B, V, N) * (det ? 8 : 4));
     L.lossp = take(BV * T * 2 * 4);  // per-tile sums of squared image / alpha residuals (fused loss)
     L.lossw = take(((BV * T + 2047) / 2048) * 16);  // their per-workgroup double2 partials (k_loss_reduce)
+    L.detmax = take(64 * 4);  // deterministic mode: max |dL/dpixel| over the seeds, in 64 atomicMax slots
     L.total = o;
     return L;
 }
@@ -371,6 +372,28 @@ __host__ __device__ __forceinline__ int xcd_group(int t, int M) {  // the block 
     return t < r * (q + 1) ? t / (q + 1) : r + (t - r * (q + 1)) / (q > 0 ? q : 1);
 }
 __host__ __device__ __forceinline__ int round8(int x) { return (x + 7) & ~7; }
+
+// Lazy tile sort (k_render_fwd): a tile's list is bucketed by depth once (histogram, scan, scatter into bucket
+// order) and then ranked chunk by chunk, only as far as its pixels composite -- about a quarter of a cfg3 tile list
+// is ever walked before every pixel saturates. The sorted ids go to the tail of the tile's slot bucket (u32 offset
+// 4n; the bucket-ordered keys take u64 [n, 2n)). Tiles outside these limits are sorted by k_sort beforehand (ids at
+// the bucket head). The predicate is workgroup-uniform and the same in k_sort, k_render_fwd, k_render_bwd and the
+// inspection copy: it depends only on the tile's list length, the workspace mode and the call's options.
+#ifndef LGM_FWD_SORT
+#define LGM_FWD_SORT 1
+#endif
+constexpr int LZ_CAP = 4096;      // longest list sorted lazily (LZ_CAP / 256 keys per thread in the bucketing pass)
+constexpr int LZ_BITS = 9, LZ_NB = 1 << LZ_BITS;  // depth buckets
+constexpr int LZ_WMAX = 448;      // window (the buckets overlapping one 256-position chunk) held in LDS
+constexpr int LZ_BMAX = (LZ_WMAX - TILE_PIX) / 2;  // larger buckets -> the in-kernel fallback (full sort)
+__host__ __device__ __forceinline__ bool lazy_tile(int n, long long slot_stride, int options) {
+    return LGM_FWD_SORT && !(options & LGM_RENDER_SORT_ALL) && slot_stride > 0 && n >= 2 && n <= LZ_CAP &&
+           5LL * n <= 2LL * slot_stride;
+}
+// the u32 offset of a tile's sorted ids from its bucket base
+__host__ __device__ __forceinline__ long long tile_ids_offset(int n, long long slot_stride, int options) {
+    return lazy_tile(n, slot_stride, options) ? 4LL * n : 0LL;
+}
 
 // Pixel of thread t inside a 16x16 tile: wavefront w owns the 8x8 quadrant (w & 1, w >> 1).
 __device__ __forceinline__ void tile_pixel(int t, int &lx, int &ly) {

@@ -96,13 +96,12 @@ int lgm_render_backward_loss(int B, int V, int N, int H, int W, const float *gau
  * lgm_render_tile_lists: tile_counts_out (DEVICE int32 [B*V*T], T = ceil(W/16)*ceil(H/16), tile-major per view)
  * receives each (view, tile)'s list length; if ids_out is not NULL, the tile's Gaussian ids in compositing
  * (depth, then id) order are copied to ids_out[offsets[bv*T + t] ...] (offsets: DEVICE int64 [B*V*T], e.g. the
- * exclusive cumsum of the counts) -- complete lists only if the forward ran with LGM_RENDER_SORT_ALL (options:
- * the forward's). Replaces reading point_list[ranges[t].x .. ranges[t].y) of the EXT.
+ * exclusive cumsum of the counts). Replaces reading point_list[ranges[t].x .. ranges[t].y) of the EXT.
  * lgm_render_pixel_state: per-pixel n_contrib (1 + list position of the last accepted entry) and final
  * transmittance, [B,V,H,W] each (DEVICE; either may be NULL). */
 int lgm_render_tile_lists(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
                           long long pair_capacity, int *tile_counts_out, const long long *offsets,
-                          unsigned *ids_out, int options, void *stream);
+                          unsigned *ids_out, void *stream);
 int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
                            long long pair_capacity, int *n_contrib_out, float *final_T_out, void *stream);
 
@@ -138,12 +137,6 @@ int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *worksp
  * lgm_render_workspace_size_opts(..., options). Pass it to forward and backward alike. */
 #define LGM_RENDER_DETERMINISTIC 16
 size_t lgm_render_workspace_size_opts(int B, int V, int N, int H, int W, long long pair_capacity, int options);
-
-/* LGM_RENDER_SORT_ALL: sort every tile list completely in the forward (what lgm_render_tile_lists reports).
- * Without it a tile list is sorted only as far as the compositing walks it (the entries behind every pixel's
- * saturation are never ordered); outputs and gradients are the same either way. Pass the same value to the
- * backward and to lgm_render_tile_lists. */
-#define LGM_RENDER_SORT_ALL 32
 
 /* LGM_RENDER_NO_CULL: bin upstream's full 3-sigma tile rects instead of dropping (Gaussian, tile) pairs where
  * alpha < 1/255 is provable for every pixel; outputs are identical either way

@@ -49,7 +49,7 @@ SIGNATURES = {
                                           _c_float, _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll,
                                           _c_int, _vp, _vp]),
     "lgm_render_tile_lists": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp,
-                                       _c_int, _vp]),
+                                       _vp]),
     "lgm_render_pixel_state": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp]),
     "lgm_gaussian_head_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp,
                                            _c_size, _vp, _vp]),
@@ -70,7 +70,6 @@ RENDER_NO_CULL = 1  # include/lgm_render.h LGM_RENDER_NO_CULL
 RENDER_CLAMP_IMAGE = 2  # include/lgm_render.h LGM_RENDER_CLAMP_IMAGE
 RENDER_BACKWARD_AGAIN = 4  # include/lgm_render.h LGM_RENDER_BACKWARD_AGAIN
 RENDER_DETERMINISTIC = 16  # include/lgm_render.h LGM_RENDER_DETERMINISTIC
-RENDER_SORT_ALL = 32  # include/lgm_render.h LGM_RENDER_SORT_ALL
 
 
 class NativeError(RuntimeError):

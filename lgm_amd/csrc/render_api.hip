@@ -56,13 +56,12 @@ __global__ __launch_bounds__(256) void k_tile_counts(int M, long long slot_strid
 __global__ __launch_bounds__(256) void k_tile_ids(long long slot_stride, const int *__restrict__ tile_start,
                                                   const int *__restrict__ tile_count,
                                                   const unsigned long long *__restrict__ pairs,
-                                                  const long long *__restrict__ offsets, unsigned *__restrict__ ids_out,
-                                                  int options) {
+                                                  const long long *__restrict__ offsets, unsigned *__restrict__ ids_out) {
     const int t = blockIdx.x;
     long long base;
     int n;
     lgm::tile_range(t, slot_stride, tile_start, tile_count, base, n);
-    const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base) + lgm::tile_ids_offset(n, slot_stride, options);
+    const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base);
     unsigned *dst = ids_out + offsets[t];
     for (int e = threadIdx.x; e < n; e += 256) dst[e] = ids[e];
 }
@@ -242,7 +241,7 @@ int lgm_render_backward_loss(int B, int V, int N, int H, int W, const float *gau
 
 int lgm_render_tile_lists(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
                           long long pair_capacity, int *tile_counts_out, const long long *offsets,
-                          unsigned *ids_out, int options, void *stream) {
+                          unsigned *ids_out, void *stream) {
     lgm::clear_error();
     lgm::Layout L;
     int rc = check_ws(B, V, N, H, W, workspace, workspace_bytes, pair_capacity, L);
@@ -259,7 +258,7 @@ int lgm_render_tile_lists(int B, int V, int N, int H, int W, const void *workspa
     LGM_LAUNCH("k_tile_counts", st, (k_tile_counts<<<(M + 255) / 256, 256, 0, st>>>(M, stride, ts, tc, tile_counts_out)));
     if (ids_out && N > 0)
         LGM_LAUNCH("k_tile_ids", st, (k_tile_ids<<<M, 256, 0, st>>>(stride, ts, tc,
-                                     (const unsigned long long *)(ws + L.pairs), offsets, ids_out, options)));
+                                     (const unsigned long long *)(ws + L.pairs), offsets, ids_out)));
     return LGM_OK;
 }
 

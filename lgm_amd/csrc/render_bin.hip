@@ -889,7 +889,7 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
 __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_RS_WPE))) void k_sort(int M, long long slot_stride, const int *__restrict__ tile_start,
                                                      const int *__restrict__ tile_count,
                                                      unsigned long long *__restrict__ pairs, int *__restrict__ order,
-                                                     unsigned long long *__restrict__ counters, int options) {
+                                                     unsigned long long *__restrict__ counters) {
     if (!LGM_XCD_ORDER && LGM_SORT_LPT == 0 && blockIdx.x == 0) {
         extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
         static_assert(RS_LDS >= (ORD_BK + RS_WAVES) * 4, "order_tiles reuses the sort image");
@@ -902,7 +902,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_
     long long base;
     int n;
     tile_range(tile, slot_stride, tile_start, tile_count, base, n);
-    if (lazy_tile(n, slot_stride, options)) return;  // k_render_fwd sorts it, as far as it composites
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     if (counters && threadIdx.x == 0) {  // per-workgroup timeline + bucket size (see lgm_diag.render_counters)
         counters[8 + 8 * (size_t)tile + 4] = t_start;
@@ -962,7 +961,7 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
             }
             LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M + (!LGM_XCD_ORDER && !LGM_SORT_LPT ? 1 : 0), RS_THREADS, RS_LDS, st>>>(
                                          (int)M, L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs,
-                                         (int *)(ws + L.order), d.counters, d.options)));
+                                         (int *)(ws + L.order), d.counters)));
         }
     }
     if (d.N == 0 && !L.slot && hipMemsetAsync(ws + L.tile_start, 0, (M + 1) * 4, st) != hipSuccess) {

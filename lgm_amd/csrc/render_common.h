@@ -28,6 +28,11 @@ constexpr int LDS_HIST_MAX = 8192;                   // tiles per view for the L
 constexpr float LOG2E = 1.4426950408889634f;
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+// Deterministic mode: every tile owns CK_QUOTA checkpoint slots (its chunk boundaries 1..CK_QUOTA), so how a tile's
+// walk splits into backward work items depends on the tile alone -- not on which tiles won the shared pool's slot
+// counters (a racing split changes the backward's per-chunk partials in their last bits). Boundaries beyond the
+// quota stay inside the previous item.
+constexpr int CK_QUOTA = 4;
 
 // Workspace layout. Pair storage `pairs` holds one u64 key (depth_bits << 32 | gaussian id) per (Gaussian, tile)
 // pair; after sorting, the tile's u32 ids are written in place at the start of its range.
@@ -38,6 +43,7 @@ struct Layout {
         accum, lossp, lossw, detmax, misc, total;
     long long cap;
     int ck_region;  // backward checkpoint slots per region (8 regions; the forward shards tiles over them)
+    int ck_slots;   // checkpoint slots in all: 8 ck_region, or CK_QUOTA per tile in deterministic mode
     bool slot;
 };
 
@@ -67,8 +73,9 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.cfin = take(BV * P * 16);  // per-pixel pre-background colour and depth totals (forward -> backward)
     // backward checkpoints (k_render_fwd -> k_render_bwd): 2 per tile on average, 5 planes of 256 floats each
     L.ck_region = (int)((2 * BV * T + 7) / 8);
-    L.ck = take((size_t)8 * L.ck_region * 5 * TILE_PIX * 4);
-    L.cklist = take((size_t)8 * L.ck_region * 8);
+    L.ck_slots = det ? (int)(CK_QUOTA * BV * T) : 8 * L.ck_region;
+    L.ck = take((size_t)L.ck_slots * 5 * TILE_PIX * 4);
+    L.cklist = take((size_t)L.ck_slots * 8);
     L.nck = take(BV * T * 4);
     L.cmask = take(BV * P);
     L.accum = take(acc_elems(B, V, N) * (det ? 8 : 4));
@@ -372,28 +379,6 @@ __host__ __device__ __forceinline__ int xcd_group(int t, int M) {  // the block 
     return t < r * (q + 1) ? t / (q + 1) : r + (t - r * (q + 1)) / (q > 0 ? q : 1);
 }
 __host__ __device__ __forceinline__ int round8(int x) { return (x + 7) & ~7; }
-
-// Lazy tile sort (k_render_fwd): a tile's list is bucketed by depth once (histogram, scan, scatter into bucket
-// order) and then ranked chunk by chunk, only as far as its pixels composite -- about a quarter of a cfg3 tile list
-// is ever walked before every pixel saturates. The sorted ids go to the tail of the tile's slot bucket (u32 offset
-// 4n; the bucket-ordered keys take u64 [n, 2n)). Tiles outside these limits are sorted by k_sort beforehand (ids at
-// the bucket head). The predicate is workgroup-uniform and the same in k_sort, k_render_fwd, k_render_bwd and the
-// inspection copy: it depends only on the tile's list length, the workspace mode and the call's options.
-#ifndef LGM_FWD_SORT
-#define LGM_FWD_SORT 1
-#endif
-constexpr int LZ_CAP = 4096;      // longest list sorted lazily (LZ_CAP / 256 keys per thread in the bucketing pass)
-constexpr int LZ_BITS = 9, LZ_NB = 1 << LZ_BITS;  // depth buckets
-constexpr int LZ_WMAX = 448;      // window (the buckets overlapping one 256-position chunk) held in LDS
-constexpr int LZ_BMAX = (LZ_WMAX - TILE_PIX) / 2;  // larger buckets -> the in-kernel fallback (full sort)
-__host__ __device__ __forceinline__ bool lazy_tile(int n, long long slot_stride, int options) {
-    return LGM_FWD_SORT && !(options & LGM_RENDER_SORT_ALL) && slot_stride > 0 && n >= 2 && n <= LZ_CAP &&
-           5LL * n <= 2LL * slot_stride;
-}
-// the u32 offset of a tile's sorted ids from its bucket base
-__host__ __device__ __forceinline__ long long tile_ids_offset(int n, long long slot_stride, int options) {
-    return lazy_tile(n, slot_stride, options) ? 4LL * n : 0LL;
-}
 
 // Pixel of thread t inside a 16x16 tile: wavefront w owns the 8x8 quadrant (w & 1, w >> 1).
 __device__ __forceinline__ void tile_pixel(int t, int &lx, int &ly) {

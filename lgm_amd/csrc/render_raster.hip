@@ -212,49 +212,6 @@ __device__ __forceinline__ void init_sentinel(Stage &S) {
     }
 }
 
-// ---- lazy tile sort (render_common.h lazy_tile): the bucketing pass and the per-chunk ranking of k_render_fwd
-struct LazySort {
-    unsigned hc[LZ_NB];                 // bucket counts -> exclusive starts -> (after the scatter) bucket ENDS
-    unsigned long long win[LZ_WMAX];    // the window being ranked: the buckets overlapping one chunk, bucket order
-    unsigned cids[2][TILE_PIX];         // sorted ids of chunk c (buffer c & 1)
-    unsigned mm[4][3];                  // per-wave key min / key max / id max
-    int flag;                           // a bucket exceeds LZ_BMAX: full sort instead
-    int wsum[4];
-};
-// The window of chunk c: sorted positions [p0, p1) lie in the buckets b_lo..b_hi, i.e. bucket-order positions
-// [start(b_lo), end(b_hi)). Every wave derives it itself from the bucket ends (no barrier): b = #buckets ending at or
-// before the position.
-__device__ __forceinline__ void lz_window(const LazySort &Z, int c, int n, int lane, int &wbeg, int &wlen) {
-    const int p0 = c * TILE_PIX, p1 = min(n, p0 + TILE_PIX) - 1;
-    int clo = 0, chi = 0;
-#pragma unroll
-    for (int q = 0; q < LZ_NB / 64; q++) {
-        const unsigned e = Z.hc[q * 64 + lane];
-        clo += __popcll(__ballot(e <= (unsigned)p0));
-        chi += __popcll(__ballot(e <= (unsigned)p1));
-    }
-    wbeg = clo ? (int)Z.hc[clo - 1] : 0;
-    wlen = (int)Z.hc[chi] - wbeg;
-}
-// rank every window entry by its composite key among its bucket's entries; those landing in chunk c's positions go
-// to cids[c & 1] (LDS) and to the tile's sorted-id tail (global, for the backward)
-__device__ __forceinline__ void lz_rank(LazySort &Z, int c, int n, int wbeg, int wlen, int shift, unsigned idmask,
-                                        unsigned *__restrict__ ids_tail) {
-    const int p0 = c * TILE_PIX, p1 = min(n, p0 + TILE_PIX);
-    for (int i = threadIdx.x; i < wlen; i += TILE_PIX) {
-        const unsigned long long x = Z.win[i];
-        const int bk = (int)(x >> shift);
-        const int bs = bk ? (int)Z.hc[bk - 1] : 0, be = (int)Z.hc[bk];
-        int rank = bs;
-        for (int z = bs - wbeg; z < be - wbeg; z++) rank += Z.win[z] < x ? 1 : 0;
-        if (rank >= p0 && rank < p1) {
-            const unsigned id = (unsigned)x & idmask;
-            Z.cids[c & 1][rank - p0] = id;
-            ids_tail[rank] = id;
-        }
-    }
-}
-
 // k_render_fwd: grid (B*V*T), block 256.
 #ifndef LGM_FWD_WPE
 #define LGM_FWD_WPE 7  // <= 72 VGPRs (spills outside the compositing loop only): 327 vs 336 us at 6, 411 at 8 (pool)
@@ -263,7 +220,7 @@ template <bool LOSS>  // LGM_RENDER_FUSED_LOSS compiled in (its epilogue registe
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE))) void k_render_fwd(Dims d, long long slot_stride, const int *__restrict__ order,
                                                     const int *__restrict__ tile_start,
                                                     const int *__restrict__ tile_count,
-                                                    unsigned long long *__restrict__ pairs,
+                                                    const unsigned long long *__restrict__ pairs,
                                                     const float4 *__restrict__ gP, const float4 *__restrict__ gQ,
                                                     const float *__restrict__ gauss,
                                                     const float *__restrict__ bg, float *__restrict__ out_img,
@@ -288,144 +245,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     long long base;
     int n;
     tile_range(tile, slot_stride, tile_start, tile_count, base, n);
-    unsigned long long *bucket = pairs + base;
-    const bool lazy = lazy_tile(n, slot_stride, d.options);  // workgroup-uniform
-    unsigned *ids_tail = reinterpret_cast<unsigned *>(bucket) + tile_ids_offset(n, slot_stride, d.options);
-    const unsigned *ids = ids_tail;  // (the bucket head when k_sort sorted the tile)
+    const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base);
     const size_t gbase = (size_t)bv * d.N;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     init_sentinel(S);
-    // ---- lazy sort: bucket the list by (depth, id) once; chunks are ranked one ahead of the compositing
-#if LGM_FWD_SORT
-    __shared__ LazySort Z;
-#endif
-    int lz_shift = 0;
-    unsigned lz_idmask = 0u;
-    bool lz_chunks = false;                 // the chunks are ranked lazily (else: the ids are already sorted)
-    unsigned long long wr0 = 0ull, wr1 = 0ull;  // the next window, in flight in registers
-    int nwbeg = 0, nwlen = 0;
-#if LGM_FWD_SORT
-    if (lazy) {
-        constexpr int R = LZ_CAP / TILE_PIX;
-        unsigned long long kv[R];
-        unsigned lmin = 0xffffffffu, lmax = 0u, imax = 0u;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const int e = r * TILE_PIX + tid;
-            kv[r] = e < n ? bucket[e] : 0ull;
-            if (e < n) {
-                const unsigned kk = (unsigned)(kv[r] >> 32);
-                lmin = min(lmin, kk);
-                lmax = max(lmax, kk);
-                imax = max(imax, (unsigned)kv[r]);
-            }
-        }
-        for (int q = tid; q < LZ_NB; q += TILE_PIX) Z.hc[q] = 0u;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            lmin = min(lmin, (unsigned)__shfl_xor((int)lmin, o, 64));
-            lmax = max(lmax, (unsigned)__shfl_xor((int)lmax, o, 64));
-            imax = max(imax, (unsigned)__shfl_xor((int)imax, o, 64));
-        }
-        if (lane == 0) { Z.mm[w][0] = lmin; Z.mm[w][1] = lmax; Z.mm[w][2] = imax; }
-        if (tid == 0) Z.flag = 0;
-        __syncthreads();
-        unsigned kmin = Z.mm[0][0], kmax = Z.mm[0][1], im = Z.mm[0][2];
-#pragma unroll
-        for (int ww = 1; ww < 4; ww++) {
-            kmin = min(kmin, Z.mm[ww][0]);
-            kmax = max(kmax, Z.mm[ww][1]);
-            im = max(im, Z.mm[ww][2]);
-        }
-        // composite key ((depth - kmin) << idb | id): one u64 compare orders (depth, id) as upstream's stable sort
-        const int idb = im ? 32 - __clz(im) : 1;
-        const int kb = (kmax - kmin) ? 32 - __clz(kmax - kmin) : 0;
-        lz_shift = max(0, kb + idb - LZ_BITS);
-        lz_idmask = idb >= 32 ? 0xffffffffu : (1u << idb) - 1u;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const int e = r * TILE_PIX + tid;
-            if (e < n) {
-                kv[r] = ((unsigned long long)((unsigned)(kv[r] >> 32) - kmin) << idb) | (unsigned)kv[r];
-                atomicAdd(&Z.hc[(int)(kv[r] >> lz_shift)], 1u);
-            }
-        }
-        __syncthreads();
-        {  // exclusive scan of the bucket counts (LZ_NB / 256 per thread) and the largest bucket
-            constexpr int BPT = LZ_NB / TILE_PIX;
-            unsigned loc[BPT], sum = 0u, mx = 0u;
-#pragma unroll
-            for (int j = 0; j < BPT; j++) {
-                loc[j] = Z.hc[tid * BPT + j];
-                sum += loc[j];
-                mx = max(mx, loc[j]);
-            }
-            unsigned incl = sum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned y = (unsigned)__shfl_up((int)incl, o, 64);
-                if (lane >= o) incl += y;
-            }
-            if (lane == 63) Z.wsum[w] = (int)incl;
-            if (mx > (unsigned)LZ_BMAX) Z.flag = 1;
-            __syncthreads();
-            unsigned run = incl - sum;
-            for (int ww = 0; ww < w; ww++) run += (unsigned)Z.wsum[ww];
-#pragma unroll
-            for (int j = 0; j < BPT; j++) {
-                Z.hc[tid * BPT + j] = run;
-                run += loc[j];
-            }
-        }
-        __syncthreads();
-        if (!Z.flag) {
-            // scatter into bucket order at bucket[n, 2n); afterwards hc[b] is bucket b's end
-            unsigned long long *scat = bucket + n;
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int e = r * TILE_PIX + tid;
-                if (e < n) scat[atomicAdd(&Z.hc[(int)(kv[r] >> lz_shift)], 1u)] = kv[r];
-            }
-            __syncthreads();  // (the scatter's global stores have completed: the windows read them back)
-            int wb, wl;
-            lz_window(Z, 0, n, lane, wb, wl);
-            for (int i = tid; i < wl; i += TILE_PIX) Z.win[i] = scat[wb + i];
-            __syncthreads();
-            lz_rank(Z, 0, n, wb, wl, lz_shift, lz_idmask, ids_tail);
-            if (n > TILE_PIX) {  // chunk 1's window: loaded now, stored once chunk 0's ranking is done
-                lz_window(Z, 1, n, lane, nwbeg, nwlen);
-                wr0 = tid < nwlen ? scat[nwbeg + tid] : 0ull;
-                wr1 = TILE_PIX + tid < nwlen ? scat[nwbeg + TILE_PIX + tid] : 0ull;
-            }
-            __syncthreads();
-            if (n > TILE_PIX) {
-                if (tid < nwlen) Z.win[tid] = wr0;
-                if (TILE_PIX + tid < nwlen) Z.win[TILE_PIX + tid] = wr1;
-            }
-            lz_chunks = true;
-        } else {
-            // clustered depths (a bucket > LZ_BMAX): a full bitonic sort of the raw keys in global memory (index >= n
-            // acts as +inf), then the ids to the tail. Rare; correct for any list.
-            int m = 1;
-            while (m < n) m <<= 1;
-            for (int kk = 2; kk <= m; kk <<= 1) {
-                for (int j = kk >> 1; j > 0; j >>= 1) {
-                    for (int p = tid; p < (m >> 1); p += TILE_PIX) {
-                        const int lo = j == (kk >> 1) ? (p / j) * kk + (p % j) : 2 * p - (p & (j - 1));
-                        const int hi = j == (kk >> 1) ? lo ^ (kk - 1) : lo + j;
-                        if (hi < n) {
-                            const unsigned long long a0 = bucket[lo], a1 = bucket[hi];
-                            if (a0 > a1) { bucket[lo] = a1; bucket[hi] = a0; }
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-            for (int e = tid; e < n; e += TILE_PIX) ids_tail[e] = (unsigned)bucket[e];
-            __syncthreads();
-        }
-    }
-#endif
     // Tr < 0 marks a saturated pixel (|Tr| its final transmittance): outside pixels start saturated
     float Tr = inside ? 1.0f : -1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     int last = 0;
@@ -437,9 +260,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     // chunks ahead in registers. Each lane tests its own entry as soon as its row has landed, so one barrier
     // publishes rows and masks together.
     constexpr int PF0 = LGM_FWD_DB == 1 ? 0 : 1;
-    static_assert(!LGM_FWD_SORT || LGM_FWD_DB == 0, "the lazy sort ranks a chunk one ahead of synchronous staging");
-    unsigned id_a = !lz_chunks && tid < n ? ids[tid] : 0u;                        // chunk c
-    unsigned id_b = !lz_chunks && TILE_PIX + tid < n ? ids[TILE_PIX + tid] : 0u;  // chunk c + 1
+    unsigned id_a = tid < n ? ids[tid] : 0u;                        // chunk c
+    unsigned id_b = TILE_PIX + tid < n ? ids[TILE_PIX + tid] : 0u;  // chunk c + 1
     int cur = 0;
     bool pre = false;  // chunk c was prefetched into S.buf[cur]
     // Backward checkpoints: entering every chunk c >= 1 the per-pixel state (T and the prefix colour / depth sums)
@@ -449,6 +271,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     // (XCD order: the region is the tile's block group and its slots are interleaved by region, so the backward's
     // checkpoint items run on the XCD that composited the tile)
     const int ck_reg = LGM_XCD_ORDER ? xcd_group(tile, d.BV * d.T) : (tile & 7);
+    const bool det_ck = (d.options & LGM_RENDER_DETERMINISTIC) != 0;  // per-tile checkpoint quota (render_common.h)
     int ck_slot = -1, ck_written = 0;  // thread 0: slot reserved for the next boundary; checkpoints written
     for (int b0 = 0, c = 0; b0 < n; b0 += TILE_PIX, c++) {
         if (tid == 0) s_ck[c & 1] = ck_slot;  // reserved during chunk c - 1 (its atomic has long returned)
@@ -456,38 +279,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         c_list += min(TILE_PIX, n - b0);
         const int k = b0 + tid;
         StageBuf &B = S.buf[cur];
-#if LGM_FWD_SORT
-        if (lz_chunks && k < n) id_a = Z.cids[c & 1][tid];  // ranked one chunk ahead
-#endif
         if (!pre && k < n) stage_dma(B, w, id_a, gbase, b, d.N, gP, gQ, gauss);
-#if LGM_FWD_SORT
-        if (lz_chunks) {
-            // while the DMA flies: rank chunk c + 1 (its window is in LDS), fetch chunk c + 2's window
-            if (b0 + TILE_PIX < n) lz_rank(Z, c + 1, n, nwbeg, nwlen, lz_shift, lz_idmask, ids_tail);
-            if (b0 + 2 * TILE_PIX < n) {
-                lz_window(Z, c + 2, n, lane, nwbeg, nwlen);
-                const unsigned long long *scat = bucket + n;
-                wr0 = tid < nwlen ? scat[nwbeg + tid] : 0ull;
-                wr1 = TILE_PIX + tid < nwlen ? scat[nwbeg + TILE_PIX + tid] : 0ull;
-            }
-        }
-#endif
         vm_wait_all();
         stage_commit(S, B, tid, k < n, 0u, tx0, ty0, false);
         __syncthreads();
-#if LGM_FWD_SORT
-        if (lz_chunks && b0 + 2 * TILE_PIX < n) {  // (every wave has ranked chunk c + 1: the window is free)
-            if (tid < nwlen) Z.win[tid] = wr0;
-            if (TILE_PIX + tid < nwlen) Z.win[TILE_PIX + tid] = wr1;
-        }
-#endif
         // checkpoint stores and the next reservation go out after this chunk's DMA wait, so they have the whole
         // chunk's compositing to complete before the next wait
         if (tid == 0) {
             ck_slot = -1;
             if (b0 + TILE_PIX < n) {
-                const unsigned l = atomicAdd(&ckctr[ck_reg], 1u);
-                if (l < (unsigned)ck_region) ck_slot = LGM_XCD_ORDER ? (int)l * 8 + ck_reg : ck_reg * ck_region + (int)l;
+                if (det_ck) {  // the tile's own quota: boundary c + 1 -> slot tile * CK_QUOTA + c
+                    if (c < CK_QUOTA) ck_slot = tile * CK_QUOTA + c;
+                } else {
+                    const unsigned l = atomicAdd(&ckctr[ck_reg], 1u);
+                    if (l < (unsigned)ck_region)
+                        ck_slot = LGM_XCD_ORDER ? (int)l * 8 + ck_reg : ck_reg * ck_region + (int)l;
+                }
             }
         }
         if (c >= 1) {
@@ -508,7 +315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         const bool pf = LGM_FWD_DB != 0 && c >= PF0 && b0 + TILE_PIX < n;  // workgroup-uniform
         if (pf && k + TILE_PIX < n) stage_dma(S.buf[cur ^ 1], w, id_b, gbase, b, d.N, gP, gQ, gauss);
         id_a = id_b;
-        id_b = !lz_chunks && k + 2 * TILE_PIX < n ? ids[k + 2 * TILE_PIX] : 0u;
+        id_b = k + 2 * TILE_PIX < n ? ids[k + 2 * TILE_PIX] : 0u;
         pre = pf;
         cur ^= pf ? 1 : 0;
         const int cnt = compact_wave(S, w, lane);
@@ -580,6 +387,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     if (LGM_FWD_DB != 0 && pre) vm_wait_all();  // no LDS DMA may be in flight when the workgroup retires
     if (tid == 0) {
         if (ck_slot >= 0) cklist[ck_slot] = make_int2(-1, 0);  // reserved for a boundary never reached
+        if (det_ck)  // the rest of the tile's quota: unused
+            for (int j = ck_written; j < CK_QUOTA; j++) cklist[tile * CK_QUOTA + j] = make_int2(-1, 0);
         nck[tile] = ck_written;  // checkpoints c = 1 .. ck_written exist (a prefix: the counters only grow)
     }
     {  // the wave's largest last contributor (outside pixels: 0), for the backward's list bounds
@@ -921,9 +730,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     } else {
         if ((int)blockIdx.x < Mp) return;  // padding: the checkpoint items start at a multiple of 8
         slot = (int)blockIdx.x - Mp;
-        const int region = LGM_XCD_ORDER ? (slot & 7) : slot / ck_region;
-        const int l = LGM_XCD_ORDER ? (slot >> 3) : slot - region * ck_region;
-        if (l >= (int)ckctr[region]) return;  // an unused slot (workgroup-uniform)
+        if (!DET) {  // (deterministic mode: every slot is written, used or not)
+            const int region = LGM_XCD_ORDER ? (slot & 7) : slot / ck_region;
+            const int l = LGM_XCD_ORDER ? (slot >> 3) : slot - region * ck_region;
+            if (l >= (int)ckctr[region]) return;  // an unused slot (workgroup-uniform)
+        }
         const int2 e = cklist[slot];
         if (e.x < 0) return;  // reserved, never written
         tile = e.x;
@@ -940,7 +751,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     long long base;
     int n;
     tile_range(tile, slot_stride, tile_start, tile_count, base, n);
-    const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base) + tile_ids_offset(n, slot_stride, d.options);
+    const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base);
 #if LGM_BWD_EARLY_STAGE
     // the first chunk's ids and LDS DMA go out before the per-pixel state loads (bounded by the list length n, a
     // superset of [s0, s1): rows past s1 are staged but never listed or flushed), so their two dependent memory
@@ -1457,7 +1268,7 @@ int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, fl
     auto fwd = (d.options & LGM_RENDER_FUSED_LOSS) ? k_render_fwd<true> : k_render_fwd<false>;
     LGM_LAUNCH("k_render_fwd", st, (fwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
-                                       (const int *)(ws + L.tile_count), (unsigned long long *)(ws + L.pairs),
+                                       (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
                                        image, depth, alpha,
                                        (float *)(ws + L.final_T), (int *)(ws + L.n_contrib), (int *)(ws + L.wlast),
@@ -1509,7 +1320,7 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
     auto bwd = d_depth ? pick(std::true_type{}) : pick(std::false_type{});
     // work items: chunk 0 of every tile, then one per checkpoint slot (unused slots exit at once)
     const int M = d.BV * d.T, Mp = LGM_XCD_ORDER ? round8(M) : M;
-    LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(Mp + 8 * L.ck_region), 256, 0, st>>>(
+    LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(Mp + L.ck_slots), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,

@@ -144,14 +144,12 @@ def deterministic_enabled() -> bool:
 
 
 def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, scale_modifier=1.0, clamp=False,
-              gt_images=None, gt_masks=None, deterministic=None, no_cull=False, sort_all=False):
+              gt_images=None, gt_masks=None, deterministic=None, no_cull=False):
     """Functional form: returns (image [B,V,3,H,W], depth [B,V,1,H,W], alpha [B,V,1,H,W]). The image is
     unclamped unless clamp=True, which applies core/gs.py:87's clamp(0, 1) (and its gradient) inside the kernels.
     With gt_images [B,V,3,H,W] and gt_masks [B,V,1,H,W] a 4th output (loss_mse, mse_image, mse_alpha, psnr) holds
     LGM's training MSE terms (core/models.py:145-148,167), fused into the kernels; it is differentiable.
-    no_cull=True bins upstream's full 3-sigma tile rects (LGM_RENDER_NO_CULL: same outputs, more work);
-    sort_all=True sorts every tile list completely instead of as far as it composites (LGM_RENDER_SORT_ALL: same
-    outputs, more work)."""
+    no_cull=True bins upstream's full 3-sigma tile rects (LGM_RENDER_NO_CULL: same outputs, more work)."""
     if not gaussians.is_cuda:  # CPU tensors: the torch path of BASELINE config 1 (lgm_amd/cpu.py), never the oracle
         from .cpu import render_cpu
         bgc = torch.as_tensor(bg, dtype=torch.float32).detach().cpu()
@@ -180,8 +178,7 @@ def rasterize(gaussians, cam_view, cam_view_proj, bg, tanfovx, tanfovy, H, W, sc
         gtm = gt_masks.to(dev, torch.float32).contiguous().detach()
         if tuple(gti.shape) != (B, V, 3, H, W) or tuple(gtm.shape) != (B, V, 1, H, W):
             raise ValueError("gt_images / gt_masks must be [B,V,3,H,W] / [B,V,1,H,W]")
-    options = (_native.RENDER_CLAMP_IMAGE if clamp else 0) | (_native.RENDER_NO_CULL if no_cull else 0) | \
-        (_native.RENDER_SORT_ALL if sort_all else 0)
+    options = (_native.RENDER_CLAMP_IMAGE if clamp else 0) | (_native.RENDER_NO_CULL if no_cull else 0)
     if deterministic_enabled() if deterministic is None else deterministic:
         options |= _native.RENDER_DETERMINISTIC
     out = _RasterizeBatched.apply(g, cv, cvp, bgt, float(tanfovx), float(tanfovy), float(scale_modifier),
@@ -216,8 +213,7 @@ def forward_state(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, sc
       radii [B,V,N] int32; K_binned / K_reference (as count_pairs); tile_counts [B,V,T] int32;
       n_contrib, final_T [B,V,H,W]; with lists=True, ids[b][v] = the view's tile lists concatenated (tile-major,
       each in compositing order). no_cull=True bins upstream's full 3-sigma rects (LGM_RENDER_NO_CULL)."""
-    # complete tile lists (the product forward sorts a list only as far as it composites it)
-    options = _native.RENDER_SORT_ALL | (_native.RENDER_NO_CULL if no_cull else 0)
+    options = _native.RENDER_NO_CULL if no_cull else 0
     L = _native.lib()
     g = gaussians.float().contiguous()
     dev = g.device
@@ -242,7 +238,7 @@ def forward_state(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, sc
     T = _tiles(H, W)
     counts = torch.empty(B * V * T, dtype=torch.int32, device=dev)
     _native.check(L.lgm_render_tile_lists(B, V, N, H, W, _native.ptr(ws), ws_bytes, 0, _native.ptr(counts), None,
-                                          None, options, stream), "lgm_render_tile_lists")
+                                          None, stream), "lgm_render_tile_lists")
     n_contrib = torch.empty(B, V, H, W, dtype=torch.int32, device=dev)
     final_T = torch.empty(B, V, H, W, dtype=torch.float32, device=dev)
     _native.check(L.lgm_render_pixel_state(B, V, N, H, W, _native.ptr(ws), ws_bytes, 0, _native.ptr(n_contrib),
@@ -257,8 +253,7 @@ def forward_state(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, sc
         total = int(c64.sum().item())
         ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
         _native.check(L.lgm_render_tile_lists(B, V, N, H, W, _native.ptr(ws), ws_bytes, 0, _native.ptr(counts),
-                                              _native.ptr(offsets), _native.ptr(ids), options, stream),
-                      "lgm_render_tile_lists")
+                                              _native.ptr(offsets), _native.ptr(ids), stream), "lgm_render_tile_lists")
         flat = ids[:total].cpu().numpy()
         per_view = c64.view(B * V, T).sum(1).tolist()
         bounds = np.concatenate([[0], np.cumsum(per_view)])

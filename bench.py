@@ -480,10 +480,18 @@ def run(args):
                 step()
             n_det = max(5, args.steps // 2)
             el_det = D.timed_steps(step, n_det, info, torch.cuda.synchronize, dev)
+            prof_d = _native.KernelProfiler()
+            with prof_d:
+                for _ in range(3):
+                    step()
+                torch.cuda.synchronize()
+            kern_d = prof_d.summary()
+            prof_d.close()
         finally:
             os.environ["LGM_AMD_DETERMINISTIC"] = "0"
         det = {"ms_per_step": round(1e3 * el_det / n_det, 4),
-               "Mpixels_per_s": round(POOL_SCENES * VIEWS * RES * RES * n_det / el_det / 1e6, 2), "steps": n_det}
+               "Mpixels_per_s": round(POOL_SCENES * VIEWS * RES * RES * n_det / el_det / 1e6, 2), "steps": n_det,
+               "kernels": {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in kern_d.items()}}
 
     P = RES * RES
     pixels = POOL_SCENES * VIEWS * P * args.steps

@@ -32,7 +32,10 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // walk splits into backward work items depends on the tile alone -- not on which tiles won the shared pool's slot
 // counters (a racing split changes the backward's per-chunk partials in their last bits). Boundaries beyond the
 // quota stay inside the previous item.
-constexpr int CK_QUOTA = 4;
+#ifndef LGM_CK_QUOTA
+#define LGM_CK_QUOTA 8
+#endif
+constexpr int CK_QUOTA = LGM_CK_QUOTA;
 
 // Workspace layout. Pair storage `pairs` holds one u64 key (depth_bits << 32 | gaussian id) per (Gaussian, tile)
 // pair; after sorting, the tile's u32 ids are written in place at the start of its range.

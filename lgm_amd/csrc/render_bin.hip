@@ -94,6 +94,40 @@ __device__ __forceinline__ int wave_incl_max(int v, int /*lane*/) {
     return v;
 }
 
+// k_sort's tile order (LGM_SORT_CENTER): the tiles of a view by distance from the image centre, nearest first.
+// The centre tiles carry the longest lists (the object sits in the middle of the frame), so with the views
+// interleaved (workgroup b sorts rank b / BV of view b % BV) the long sorts start in the first residency round and
+// the short ones fill the second. One binning workgroup writes it at its end: a counting sort of the tiles on their
+// squared centre distance quantised to min(T, BIN_THREADS) buckets, in LDS (hk: >= that + RS-wave sums ints). Ties
+// take atomic slots -- the order only schedules the sorts, every order gives the same result.
+#ifndef LGM_SORT_CENTER
+#define LGM_SORT_CENTER 1
+#endif
+__device__ void center_order(int gx, int T, int *__restrict__ corder, int *hk) {
+    const int gy = (T + gx - 1) / gx, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int K = min(T, BIN_THREADS);
+    const long long maxkey = (long long)(gx - 1) * (gx - 1) + (long long)(gy - 1) * (gy - 1);
+    auto key = [&](int t) {
+        const int y = t / gx, x = t - y * gx, dx = 2 * x - (gx - 1), dy = 2 * y - (gy - 1);
+        return maxkey ? (int)(((long long)dx * dx + (long long)dy * dy) * (K - 1) / maxkey) : 0;
+    };
+    __syncthreads();  // (hk is the binning histogram's LDS)
+    if (tid < K) hk[tid] = 0;
+    __syncthreads();
+    for (int t = tid; t < T; t += BIN_THREADS) atomicAdd(&hk[key(t)], 1);
+    __syncthreads();
+    const int v = tid < K ? hk[tid] : 0;
+    const int incl = wave_incl_scan(v, lane);
+    if (lane == 63) hk[K + w] = incl;
+    __syncthreads();
+    int run = incl - v;
+    for (int ww = 0; ww < w; ww++) run += hk[K + ww];
+    __syncthreads();
+    if (tid < K) hk[tid] = run;
+    __syncthreads();
+    for (int t = tid; t < T; t += BIN_THREADS) corder[atomicAdd(&hk[key(t)], 1)] = t;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__restrict__ gauss, const float *__restrict__ views,
                                                      const float *__restrict__ projs, float4 *__restrict__ gP,
@@ -101,7 +135,8 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                                                      uint2 *__restrict__ rects, int *__restrict__ radii_out,
                                                      int *__restrict__ tile_count, const int *__restrict__ tile_start,
                                                      unsigned long long *__restrict__ pairs, long long slot_stride,
-                                                     unsigned long long *__restrict__ misc, float *__restrict__ accum) {
+                                                     unsigned long long *__restrict__ misc, float *__restrict__ accum,
+                                                     int *__restrict__ corder) {
     extern __shared__ int hist[];  // [T] per-tile hit counts, [T] reserved global bases, [T] fallback cursors
     __shared__ BinRec srec[BIN_THREADS];
     __shared__ int sHead[BIN_THREADS], sExcl[BIN_THREADS];
@@ -350,6 +385,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         atomicAdd(&misc[0], s_tot[0]);
         atomicAdd(&misc[1], s_tot[1]);
     }
+    if (corder && blockIdx.x == 0 && blockIdx.y == 0) center_order(d.gx, T, corder, hist);
 }
 
 // k_scan: one workgroup of 1024 threads; exclusive scan of the M tile counts -> tile_start[0..M].
@@ -889,7 +925,8 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
 __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_RS_WPE))) void k_sort(int M, long long slot_stride, const int *__restrict__ tile_start,
                                                      const int *__restrict__ tile_count,
                                                      unsigned long long *__restrict__ pairs, int *__restrict__ order,
-                                                     unsigned long long *__restrict__ counters) {
+                                                     unsigned long long *__restrict__ counters, int BV, int T,
+                                                     const int *__restrict__ corder) {
     if (!LGM_XCD_ORDER && LGM_SORT_LPT == 0 && blockIdx.x == 0) {
         extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
         static_assert(RS_LDS >= (ORD_BK + RS_WAVES) * 4, "order_tiles reuses the sort image");
@@ -898,7 +935,11 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_
         return;
     }
     // LGM_SORT_LPT: k_order ran first and the sorts take their tiles longest first too
-    const int tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, M) : LGM_SORT_LPT ? order[blockIdx.x] : (int)blockIdx.x - 1;
+    int tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, M) : LGM_SORT_LPT ? order[blockIdx.x] : (int)blockIdx.x - 1;
+    if (corder) {  // centre-first, views interleaved (center_order)
+        const int r = (int)blockIdx.x / BV, v = (int)blockIdx.x - r * BV;
+        tile = v * T + corder[r];
+    }
     long long base;
     int n;
     tile_range(tile, slot_stride, tile_start, tile_count, base, n);
@@ -932,6 +973,9 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     unsigned long long *pairs = (unsigned long long *)(ws + L.pairs), *misc = (unsigned long long *)(ws + L.misc);
     float *accum = (float *)(ws + L.accum);
     const size_t lds = d.T <= LDS_HIST_MAX ? 3 * (size_t)d.T * 4 : 0;
+    // k_sort's centre-first tile table (first T ints of the order buffer, which the XCD order leaves unused; the
+    // binning histogram's 3T ints of LDS hold its counting sort)
+    int *corder = LGM_SORT_CENTER && LGM_XCD_ORDER && lds && d.T >= 8 ? (int *)(ws + L.order) : nullptr;
 #if LGM_BIN_VIEWLOOP
     dim3 grid((d.N + BIN_G - 1) / BIN_G, d.B * ((d.V + BIN_ITERS - 1) / BIN_ITERS));
 #else
@@ -940,12 +984,12 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     if (d.N > 0) {
         if (count_only || !L.slot) {
             LGM_LAUNCH("k_bin_count", st, (k_bin<COUNT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
-                       gP, gQ, rects, nullptr, tcount, tstart, pairs, 0, misc, accum)));
+                       gP, gQ, rects, nullptr, tcount, tstart, pairs, 0, misc, accum, nullptr)));
         }
         if (!count_only) {
             if (L.slot) {
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_SLOT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
-                           gP, gQ, rects, radii_out, tcount, tstart, pairs, (long long)d.N, misc, accum)));
+                           gP, gQ, rects, radii_out, tcount, tstart, pairs, (long long)d.N, misc, accum, corder)));
             } else {
                 LGM_LAUNCH("k_scan", st, (k_scan<<<1, 1024, 0, st>>>(tcount, (int)M, tstart)));
                 if (hipMemsetAsync(ws + L.tile_count, 0, L.misc + 64 - L.tile_count, st) != hipSuccess) {
@@ -953,7 +997,7 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                     return LGM_E_HIP;
                 }
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view,
-                           cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum)));
+                           cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum, corder)));
             }
             if (!LGM_XCD_ORDER && LGM_SORT_LPT) {
                 LGM_LAUNCH("k_order", st, (k_order<<<1, ORD_THREADS, 0, st>>>((int)M, L.slot ? (long long)d.N : -1LL,
@@ -961,7 +1005,7 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
             }
             LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M + (!LGM_XCD_ORDER && !LGM_SORT_LPT ? 1 : 0), RS_THREADS, RS_LDS, st>>>(
                                          (int)M, L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs,
-                                         (int *)(ws + L.order), d.counters)));
+                                         (int *)(ws + L.order), d.counters, d.BV, d.T, corder)));
         }
     }
     if (d.N == 0 && !L.slot && hipMemsetAsync(ws + L.tile_start, 0, (M + 1) * 4, st) != hipSuccess) {

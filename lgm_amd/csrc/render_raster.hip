@@ -93,6 +93,9 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #ifndef LGM_BWD_PIPE
 #define LGM_BWD_PIPE 1  // software-pipelined moment flush (k_render_bwd): batch k's MFMAs overlap batch k + 1's evaluation
 #endif
+#ifndef LGM_BWD_CENTER
+#define LGM_BWD_CENTER 0  // head work items in k_bin's centre-first order instead of the XCD order
+#endif
 #ifndef LGM_BWD_CHUNK
 #define LGM_BWD_CHUNK 64  // backward entries per staged chunk (the per-wave moment slots scale with it)
 #endif
@@ -727,6 +730,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     int tile, c = 0, slot = -1;
     if ((int)blockIdx.x < M) {
         tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, M) : order[blockIdx.x];
+#if LGM_BWD_CENTER
+        if (LGM_XCD_ORDER && d.T >= 8 && d.T <= LDS_HIST_MAX) {  // centre-first head items (k_bin's centre order)
+            const int r = (int)blockIdx.x / d.BV, v = (int)blockIdx.x - r * d.BV;
+            tile = v * d.T + order[r];
+        }
+#endif
     } else {
         if ((int)blockIdx.x < Mp) return;  // padding: the checkpoint items start at a multiple of 8
         slot = (int)blockIdx.x - Mp;
@@ -1113,6 +1122,10 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
     const int det_s = det ? det_seed_shift(det_max) : 0;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
+    // diagnostics: workgroup g's start / end in slots [2], [3] of per-tile record g (unused by the other kernels)
+    const size_t g_diag = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const bool stamp = d.counters && threadIdx.x == 0 && g_diag < (size_t)d.BV * d.T;
+    if (stamp) d.counters[8 + 8 * g_diag + 2] = __builtin_amdgcn_s_memrealtime();
     if (i >= d.N) return;
     const float fx = d.fx, fy = d.fy, mod = d.mod;
     float g[14];
@@ -1258,6 +1271,7 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
     float2 *o2 = reinterpret_cast<float2 *>(o);
 #pragma unroll
     for (int kk = 0; kk < 7; kk++) o2[kk] = make_float2(out[2 * kk], out[2 * kk + 1]);
+    if (stamp) d.counters[8 + 8 * g_diag + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
 }  // namespace

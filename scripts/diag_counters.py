@@ -41,7 +41,7 @@ res["tile_list_max"] = int(nl.max())
 res["tile_list_p50"] = float(np.median(nl))
 res["tile_list_mean"] = float(nl.mean())
 res["tile_list_hist_1k"] = np.bincount(nl // 1024).tolist()
-for name, (a, b) in {"fwd": (0, 1), "bwd": (2, 3), "sort": (4, 5)}.items():
+for name, (a, b) in {"fwd": (0, 1), "preproc_bwd": (2, 3), "sort": (4, 5)}.items():
     st, en = tl[:, a], tl[:, b]
     ok = en > 0
     if not ok.any():  # no per-workgroup timeline for this kernel (the backward records none)

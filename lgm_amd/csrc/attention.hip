@@ -796,7 +796,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
     ld_.store(Ks[0], Vs[0], LDK);
     __syncthreads();
     int cur = 0;
-    for (int kb = 0; kb < L; kb += 64) {
+    // one 64-key tile; TAIL: the last, partial tile (keys >= L masked) -- full tiles run a body without the masking
+    // (a runtime tail flag left ~70 compare / select VALU per tile in the main loop)
+    auto step = [&](int kb, auto tail_tag) {
+        constexpr bool TAIL = decltype(tail_tag)::value;
         const bool more = kb + 64 < L;
         if (more) ld_.load(k + base, ld, v + base, ld, kb + 64, L);
         const T *Kt = Ks[cur], *Vt = Vs[cur];
@@ -821,13 +824,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
                 dpa[s][sub] = dp;
             }
         }
-        const bool tail = kb + 64 > L;
         V8 db[QS][2];
 #pragma unroll
         for (int sub = 0; sub < 4; sub++)
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const bool kv = !tail || kb + 16 * sub + 4 * g + i < L;
+                const bool kv = !TAIL || kb + 16 * sub + 4 * g + i < L;
 #pragma unroll
                 for (int s = 0; s < QS; s++) {
                     const float p = kv ? __builtin_amdgcn_exp2f(fmaf(sacc[s][sub][i], c, -l2[s])) : 0.f;
@@ -845,7 +847,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
         if (more) ld_.store(Ks[cur ^ 1], Vs[cur ^ 1], LDK);
         __syncthreads();
         cur ^= 1;
-    }
+    };
+    const int kfull = L & ~63;
+    for (int kb = 0; kb < kfull; kb += 64) step(kb, std::false_type{});
+    if (kfull < L) step(kfull, std::true_type{});
 #pragma unroll
     for (int s = 0; s < QS; s++) {
         const int qr = q0 + 16 * s + r16;

@@ -93,9 +93,6 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #ifndef LGM_BWD_PIPE
 #define LGM_BWD_PIPE 1  // software-pipelined moment flush (k_render_bwd): batch k's MFMAs overlap batch k + 1's evaluation
 #endif
-#ifndef LGM_BWD_CENTER
-#define LGM_BWD_CENTER 0  // head work items in k_bin's centre-first order instead of the XCD order
-#endif
 #ifndef LGM_BWD_CHUNK
 #define LGM_BWD_CHUNK 64  // backward entries per staged chunk (the per-wave moment slots scale with it)
 #endif
@@ -730,12 +727,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     int tile, c = 0, slot = -1;
     if ((int)blockIdx.x < M) {
         tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, M) : order[blockIdx.x];
-#if LGM_BWD_CENTER
-        if (LGM_XCD_ORDER && d.T >= 8 && d.T <= LDS_HIST_MAX) {  // centre-first head items (k_bin's centre order)
-            const int r = (int)blockIdx.x / d.BV, v = (int)blockIdx.x - r * d.BV;
-            tile = v * d.T + order[r];
-        }
-#endif
     } else {
         if ((int)blockIdx.x < Mp) return;  // padding: the checkpoint items start at a multiple of 8
         slot = (int)blockIdx.x - Mp;
@@ -1110,7 +1101,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     }
 }
 
-// k_preproc_bwd: grid (ceil(N/256), B), block 256. Sums over the scene's views in order (deterministic).
+// k_preproc_bwd: grid (ceil(N/256), B), block 256. Sums over the scene's views in order (deterministic; the
+// order must not depend on the launch's size: a batched pool equals its scenes rendered alone, bit for bit).
 __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__restrict__ gauss,
                                                      const float *__restrict__ views,
                                                      const float *__restrict__ projs, const uint2 *__restrict__ rects,

@@ -31,9 +31,8 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // Deterministic mode: every tile owns CK_QUOTA checkpoint slots (its chunk boundaries 1..CK_QUOTA), so how a tile's
 // walk splits into backward work items depends on the tile alone -- not on which tiles won the shared pool's slot
 // counters (a racing split changes the backward's per-chunk partials in their last bits). Boundaries beyond the
-// quota stay inside the previous item. Default 0: one backward item per tile. Every quota slot is a launched
-// backward workgroup, used or not (most tiles need none), and those cost more than the split's load balance returns --
-// measured on the pool (profiles/r03/ab_det):
+// quota stay inside the previous item. Default 0: one backward item per tile -- in this mode the split costs more
+// than its load balance returns, measured on the pool (profiles/r03/ab_det):
 // deterministic k_render_bwd 1950 / 1306 / 955 / 787 / 685 / 650 us at quota 16 / 8 / 4 / 2 / 1 / 0 (float mode 626).
 #ifndef LGM_CK_QUOTA
 #define LGM_CK_QUOTA 0

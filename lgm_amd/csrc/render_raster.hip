@@ -1101,6 +1101,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     }
 }
 
+// The preprocess backward's recomputation of the forward's projection (make_proj / cov2d / the homogeneous
+// divide): FP contraction on and 1-ulp v_rcp_f32 reciprocals. The forward keeps the oracle's bit-exact operation
+// order because its integer outputs (radii, tile rects, sort keys) depend on it; here the values only feed
+// gradients, and each IEEE division is ~10 VALU of a single thread's serial view chain.
+#ifndef LGM_PREPROC_FAST
+#define LGM_PREPROC_FAST 1
+#endif
+__device__ __forceinline__ ProjCtx make_proj_bwd(const float *Vw, float mx, float my, float mz, float fx, float fy,
+                                                 float tanx, float tany) {
+    ProjCtx P;
+    P.t[0] = Vw[0] * mx + Vw[4] * my + Vw[8] * mz + Vw[12];
+    P.t[1] = Vw[1] * mx + Vw[5] * my + Vw[9] * mz + Vw[13];
+    P.t[2] = Vw[2] * mx + Vw[6] * my + Vw[10] * mz + Vw[14];
+    const float limx = 1.3f * tanx, limy = 1.3f * tany, rtz = __builtin_amdgcn_rcpf(P.t[2]);
+    const float txtz = P.t[0] * rtz, tytz = P.t[1] * rtz;
+    P.t[0] = fminf(limx, fmaxf(-limx, txtz)) * P.t[2];
+    P.t[1] = fminf(limy, fmaxf(-limy, tytz)) * P.t[2];
+    P.xmul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+    P.ymul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+    const float J00 = fx * rtz, J02 = -(fx * P.t[0]) * rtz * rtz;
+    const float J11 = fy * rtz, J12 = -(fy * P.t[1]) * rtz * rtz;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        P.T0[r] = Vw[4 * r + 0] * J00 + Vw[4 * r + 2] * J02;
+        P.T1[r] = Vw[4 * r + 1] * J11 + Vw[4 * r + 2] * J12;
+    }
+    return P;
+}
+__device__ __forceinline__ void cov2d_bwd(const ProjCtx &P, const float c3[6], float &a, float &b, float &c) {
+    const float S[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
+    float s0[3], s1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        s0[k] = S[k][0] * P.T0[0] + S[k][1] * P.T0[1] + S[k][2] * P.T0[2];
+        s1[k] = S[k][0] * P.T1[0] + S[k][1] * P.T1[1] + S[k][2] * P.T1[2];
+    }
+    a = P.T0[0] * s0[0] + P.T0[1] * s0[1] + P.T0[2] * s0[2] + 0.3f;
+    b = s1[0] * P.T0[0] + s1[1] * P.T0[1] + s1[2] * P.T0[2];
+    c = P.T1[0] * s1[0] + P.T1[1] * s1[1] + P.T1[2] * s1[2] + 0.3f;
+}
+
 // k_preproc_bwd: grid (ceil(N/256), B), block 256. Sums over the scene's views in order (deterministic; the
 // order must not depend on the launch's size: a batched pool equals its scenes rendered alone, bit for bit).
 __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__restrict__ gauss,
@@ -1166,12 +1207,20 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         const float *Vw = views + 16 * bv;
         const float *Pm = projs + 16 * bv;
         // ---- cov2D backward
+#if LGM_PREPROC_FAST
+        const ProjCtx Pc = make_proj_bwd(Vw, g[0], g[1], g[2], fx, fy, d.tanx, d.tany);
+        float a, bb, c;
+        cov2d_bwd(Pc, c3, a, bb, c);
+        const float denom = a * c - bb * bb;
+        const float denom2inv = __builtin_amdgcn_rcpf((denom * denom) + 0.0000001f);
+#else
         const ProjCtx Pc = make_proj(Vw, g[0], g[1], g[2], fx, fy, d.tanx, d.tany);
         float a, bb, c;
         cov2d(Pc, c3, a, bb, c);
         const float denom = a * c - bb * bb;
-        float dL_da = 0, dL_db = 0, dL_dc = 0;
         const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+#endif
+        float dL_da = 0, dL_db = 0, dL_dc = 0;
         if (denom2inv != 0) {
             dL_da = denom2inv * (-c * c * dcx + 2 * bb * c * dcy + (denom - a * c) * dcz);
             dL_dc = denom2inv * (-a * a * dcz + 2 * a * bb * dcy + (denom - a * c) * dcx);
@@ -1196,7 +1245,7 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         const float dJ02 = Vw[2] * dT0[0] + Vw[6] * dT0[1] + Vw[10] * dT0[2];
         const float dJ11 = Vw[1] * dT1[0] + Vw[5] * dT1[1] + Vw[9] * dT1[2];
         const float dJ12 = Vw[2] * dT1[0] + Vw[6] * dT1[1] + Vw[10] * dT1[2];
-        const float tz = 1.f / Pc.t[2], tz2 = tz * tz, tz3 = tz2 * tz;
+        const float tz = LGM_PREPROC_FAST ? __builtin_amdgcn_rcpf(Pc.t[2]) : 1.f / Pc.t[2], tz2 = tz * tz, tz3 = tz2 * tz;
         const float dtx = Pc.xmul * -fx * tz2 * dJ02;
         const float dty = Pc.ymul * -fy * tz2 * dJ12;
         const float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * Pc.t[0]) * tz3 * dJ02 +
@@ -1206,8 +1255,15 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         dmean[2] += Vw[8] * dtx + Vw[9] * dty + Vw[10] * dtz;
         // ---- perspective-divide backward
         float hom[4];
+#if LGM_PREPROC_FAST
+        hom[0] = Pm[0] * g[0] + Pm[4] * g[1] + Pm[8] * g[2] + Pm[12];
+        hom[1] = Pm[1] * g[0] + Pm[5] * g[1] + Pm[9] * g[2] + Pm[13];
+        hom[3] = Pm[3] * g[0] + Pm[7] * g[1] + Pm[11] * g[2] + Pm[15];
+        const float m_w = __builtin_amdgcn_rcpf(hom[3] + 0.0000001f);
+#else
         xf44(Pm, g[0], g[1], g[2], hom);
         const float m_w = 1.0f / (hom[3] + 0.0000001f);
+#endif
         const float mul1 = hom[0] * m_w * m_w;
         const float mul2 = hom[1] * m_w * m_w;
         dmean[0] += (Pm[0] * m_w - Pm[3] * mul1) * dm2x + (Pm[1] * m_w - Pm[3] * mul2) * dm2y;

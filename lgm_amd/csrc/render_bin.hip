@@ -251,12 +251,13 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         if (o.tau >= 3.0e38f || !(detq > 0.f) || !(o.A > 0.f) || !(o.C > 0.f)) {  // never culled: whole rows
             r.kB = 0.f; r.k0 = INFINITY; r.k1 = 0.f; r.dys = 0.f; r.mg = 0.f;
         } else {
-            const float iA = 1.0f / o.A;
+            // (1-ulp reciprocals: the interval ends carry the margin mg, far above their rounding)
+            const float iA = __builtin_amdgcn_rcpf(o.A);
             r.kB = o.B * iA;
             r.k0 = fmaxf(o.tau, 0.f) * iA;
             r.k1 = detq * iA * iA;
-            const float hxe = sqrtf(fmaxf(o.tau, 0.f) * o.C / detq);
-            r.dys = -o.B * hxe / o.C;
+            const float hxe = sqrtf(fmaxf(o.tau, 0.f) * o.C * __builtin_amdgcn_rcpf(detq));
+            r.dys = -o.B * hxe * __builtin_amdgcn_rcpf(o.C);
             r.mg = 1e-3f * hxe + 1e-2f;  // >> the fp32 error of the interval ends (sqrt cancellation at the edge)
         }
         r.c0 = (unsigned)o.cx0 | ((unsigned)o.cy0 << 16);

@@ -318,14 +318,15 @@ __device__ __forceinline__ bool preprocess_one(const float *g, const float *Vw, 
     // fp32 evaluation of q = A dx^2 + 2B dx dy + C dy^2 loses ~eps * kappa relative accuracy on elongated
     // ellipses; cond = (a + c)^2 / det ~ kappa. Inflate tau by 1e-3 + 2e-5 * cond (>= 80x the rounding bound) and
     // do not cull ill-conditioned or non-positive-definite ones at all (keep upstream's full rect).
-    const float cond = (a + c) * (a + c) / det;
+    const float cond = (a + c) * (a + c) * __builtin_amdgcn_rcpf(det);  // (a threshold: 1 ulp is immaterial)
     if (!(det > 0.f) || !(cond < 4e4f)) {
         o.hx = o.hy = 3.0e38f;
         o.tau = 3.0e38f;
         o.cx0 = x0; o.cx1 = x1; o.cy0 = y0; o.cy1 = y1;
         return true;
     }
-    const float tau = 2.0f * logf(255.0f * op) * (1.001f + 2e-5f * cond) + 1e-3f;
+    // 2 ln(255 o) by v_log_f32 (log2, ~1 ulp): the 1e-3 inflation dwarfs it
+    const float tau = (2.0f * 0.6931471805599453f) * __builtin_amdgcn_logf(255.0f * op) * (1.001f + 2e-5f * cond) + 1e-3f;
     o.tau = tau;
     o.hx = sqrtf(tau * fmaxf(a, 0.f));
     o.hy = sqrtf(tau * fmaxf(c, 0.f));

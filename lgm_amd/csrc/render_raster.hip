@@ -110,9 +110,14 @@ __device__ __forceinline__ void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F7
 // would wait for the prefetch right after issuing it. Hidden from the pass, the DMA only makes the pass's own
 // vmcnt waits more conservative (still correct); its completion is ordered explicitly by vm_wait_all() plus a
 // barrier. M0 is saved and restored around it (the compiler owns M0), with the M0 -> LDS-DMA wait state.
+// The LDS address of a shared-memory pointer as a 32-bit offset (an address-space cast, not the 64-bit flat pointer:
+// kept live across the staging loop, the flat pointers were spilled and each reload's vmcnt(0) serialised the DMAs).
+__device__ __forceinline__ unsigned lds_offset(const void *p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
 template <int BYTES>
-__device__ __forceinline__ void lds_dma(const void *src, void *lds_row0) {
-    const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_row0);
+__device__ __forceinline__ void lds_dma(const void *src, unsigned lds_row0) {
+    const unsigned m = __builtin_amdgcn_readfirstlane(lds_row0);
     unsigned saved;
     if (BYTES == 16)
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\t"
@@ -134,9 +139,11 @@ template <class Buf>
 __device__ __forceinline__ void stage_dma(Buf &B, int w, unsigned gid, size_t gbase, int b, int N,
                                           const float4 *__restrict__ gP, const float4 *__restrict__ gQ,
                                           const float *__restrict__ gauss) {
-    lds_dma<16>(gP + gbase + gid, &B.P[w * 64]);
-    lds_dma<16>(gQ + gbase + gid, &B.Q[w * 64]);
-    lds_dma<12>(gauss + ((size_t)b * N + gid) * 14 + 11, &B.R[w * 64]);
+    // one 32-bit LDS base, the three rows at constant offsets from it
+    const unsigned base = lds_offset(&B) + (unsigned)(w * 64 * 16);
+    lds_dma<16>(gP + gbase + gid, base + (unsigned)offsetof(Buf, P));
+    lds_dma<16>(gQ + gbase + gid, base + (unsigned)offsetof(Buf, Q));
+    lds_dma<12>(gauss + ((size_t)b * N + gid) * 14 + 11, base + (unsigned)offsetof(Buf, R));
 }
 
 // Entry j of a landed chunk: its quadrant mask (the alpha >= 1/255 ellipse against the four 8x8 quadrants) and,

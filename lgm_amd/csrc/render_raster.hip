@@ -93,6 +93,10 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #ifndef LGM_BWD_PIPE
 #define LGM_BWD_PIPE 1  // software-pipelined moment flush (k_render_bwd): batch k's MFMAs overlap batch k + 1's evaluation
 #endif
+#ifndef LGM_BWD_FLUSH_WAVES
+#define LGM_BWD_FLUSH_WAVES 0  // 1: the gradient atomics on waves 1-3 only, the staging wait on wave 0 only
+                               // (measured slower: 622 -> 694 us on the pool, profiles/r03/ab_bwd_flush)
+#endif
 #ifndef LGM_BWD_CHUNK
 #define LGM_BWD_CHUNK 64  // backward entries per staged chunk (the per-wave moment slots scale with it)
 #endif
@@ -808,6 +812,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     }
 #endif
     const unsigned long long t_item = d.counters ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#ifdef LGM_BWD_STAMPS  // section cycles of this wave (diagnostic build; counters [2..6], scripts/diag_bwd_stamps.py)
+    unsigned long long sec[5] = {0, 0, 0, 0, 0};
+    SEC_T(ts_item);
+#endif
     const float bg_dot = bg[0] * dp0 + bg[1] * dp1 + bg[2] * dp2;
     float cdpf = fmaf(cf.x, dp0, fmaf(cf.y, dp1, cf.z * dp2));
     if (DEPTH) cdpf = fmaf(cf.w, dpd, cdpf);
@@ -919,7 +927,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #endif
     vm_wait_all();
     int cur = 0;
+#ifdef LGM_BWD_STAMPS
+    SEC_T(ts_loop);
+    SEC_ADD(sec[0], ts_item, ts_loop);  // prologue: pixel state, seeds, MFMA operands, first staging
+#endif
     for (int b0 = s0; b0 < s1; b0 += CH, cur ^= 1) {
+#ifdef LGM_BWD_STAMPS
+        SEC_T(ts_c0);
+#endif
         __syncthreads();
         const int k = b0 + tid;
         auto &B = S.buf[cur];
@@ -964,6 +979,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         const int cnt = compact_wave(S, w, lane, 0, wlast - b0);  // positions < wlast only
 #endif
         static_assert(MB == 8, "one batch = two 4-entry list words");
+#ifdef LGM_BWD_STAMPS
+        SEC_T(ts_c1);
+        SEC_ADD(sec[1], ts_c0, ts_c1);  // chunk head: barriers, quadrant tests + compaction, next DMA issue
+#endif
         const int lastrel = last - b0;  // this pixel's last contributor, relative to the chunk
         uint2 lraw[2];  // the next step's list words, read one step ahead
         list_raw<MB>(S, w, 0, lraw);
@@ -1037,6 +1056,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             flush_batch();
         }
 #endif
+#ifdef LGM_BWD_STAMPS
+        SEC_T(ts_c2);
+        SEC_ADD(sec[2], ts_c1, ts_c2);  // the entries loop (evaluation, moments)
+#endif
         __syncthreads();
         // moments -> gradient partials (one thread per staged entry): the sum over the four waves' slots,
         // converted, into wave 0's slots
@@ -1078,19 +1101,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #pragma unroll
             for (int qq = 0; qq < NV; qq++) o[qq * LS + j] = part[qq];
         }
-        vm_wait_all();  // the next chunk's DMA and ids have landed: the atomics below cannot delay them
+#ifdef LGM_BWD_STAMPS
+        SEC_T(ts_c3);
+        SEC_ADD(sec[3], ts_c2, ts_c3);  // barrier + moments -> partials
+#endif
+        // the next chunk's DMA and ids have landed before the atomics below go out (they cannot delay it).
+        // LGM_BWD_FLUSH_WAVES: only wave 0 -- the stager -- waits, and only waves 1-3 issue the atomics: vmcnt is
+        // per wave and in order, so a wave that issued atomics would wait for them too at the next DMA wait
+        if (!LGM_BWD_FLUSH_WAVES || w == 0) vm_wait_all();
         __syncthreads();
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
+        constexpr int FT = LGM_BWD_FLUSH_WAVES ? 192 : 256;  // flushing threads
+        const int ft = LGM_BWD_FLUSH_WAVES ? tid - 64 : tid;
 #pragma unroll
-        for (int it = 0; it < (CH * NACC + 255) / 256; it++) {
-            const int f = it * 256 + tid;
+        for (int it = 0; it < (CH * NACC + FT - 1) / FT; it++) {
+            const int f = it * FT + ft;
             const int j = f / NACC, q = f - j * NACC;
-            if (q < NV && j < CH && b0 + j < s1) {
+            if (ft >= 0 && q < NV && j < CH && b0 + j < s1) {
                 const float a = sAccW[0][q * LS + j];
                 const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
                 const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
+#ifdef LGM_TIMING_NO_ATOMICS  // timing-only build: the flush's atomics become plain stores of the same shape
+                if (a != 0.f) accum[ai] = a;
+                if (false) {
+#else
                 if (a != 0.f) {
+#endif
                     if (DET)  // integer adds commute: order-independent sums (a is already in fixed-point units)
                         atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
                                   (unsigned long long)__float2ll_rn(fminf(fmaxf(a, -9.0e18f), 9.0e18f)));
@@ -1099,7 +1136,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 }
             }
         }
+#ifdef LGM_BWD_STAMPS
+        SEC_T(ts_c4);
+        SEC_ADD(sec[4], ts_c3, ts_c4);  // DMA wait + barrier + gradient atomics
+#endif
     }
+#ifdef LGM_BWD_STAMPS
+    if (d.counters && lane == 0)
+#pragma unroll
+        for (int q = 0; q < 5; q++) atomicAdd(&d.counters[2 + q], sec[q]);
+#endif
     if (d.counters && tid == 0) {  // work-item timeline (lgm_diag.render_counters): start, end, (length | chunk | tile)
         unsigned long long *o = d.counters + item_stamps + 4 * (size_t)blockIdx.x;
         o[0] = t_item;

@@ -12,14 +12,16 @@ from lgm_amd.cameras import orbit_cameras  # noqa: E402
 from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads  # noqa: E402
 
 dev = torch.device("cuda:0")
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1  # 1: cfg3 (seed 1); 8: bench.py's pool (seed 2)
 r = GaussianRenderer(Options(output_size=256))
-g = synthetic_gaussians(1, 100000, seed=1).to(dev).requires_grad_(True)
-cv, cvp, cp = orbit_cameras(6)
-d_img, _, d_alpha, bg = synthetic_upstream_grads(1, 6, 256, 256, seed=1001)
+g = synthetic_gaussians(B, 100000, seed=1 if B == 1 else 2).to(dev).requires_grad_(True)
+cv, cvp, cp = (t[None].expand(B, *t.shape).contiguous().to(dev) for t in orbit_cameras(6))
+d_img, _, d_alpha, bg = synthetic_upstream_grads(B, 6, 256, 256, seed=1001 if B == 1 else 1002)
 L = _native.lib()
-cnt = torch.zeros(8 + 8 * 6 * 256 + 8 * 6 * 200 + 4 * 5 * 6 * 256, dtype=torch.int64, device=dev)
+M = B * 6 * 256
+cnt = torch.zeros(8 + 8 * M + 8 * B * 6 * 200 + 4 * 5 * M, dtype=torch.int64, device=dev)
 for it in range(6):
-    o = r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev), bg_color=bg.to(dev))
+    o = r.render(g, cv, cvp, cp, bg_color=bg.to(dev))
     torch.cuda.synchronize()
     if it == 5:
         cnt.zero_()
@@ -28,8 +30,8 @@ for it in range(6):
         torch.cuda.synchronize()
     g.grad = None
 c = cnt[:10].tolist()
-names = ["stage", "compact", "entries", "flush", "tail"]
+names = ["prologue", "chunk_head", "entries", "partials", "flush"]
 tot = sum(c[2:7])
 res = {n: {"Gcyc": round(v / 1e9, 3), "share": round(v / max(tot, 1), 3)} for n, v in zip(names, c[2:7])}
-res["quadrant_imbalance_max_over_mean"] = round(c[9] / max(c[8], 1), 3)
+res["B"] = B
 print(json.dumps(res))

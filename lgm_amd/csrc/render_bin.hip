@@ -7,10 +7,11 @@
 //                      tile it can reach (LDS tile histogram -> one global atomic reservation per touched tile per
 //                      workgroup -> LDS-local positions). Slot buckets need no count pass and no scan.
 //   k_bin<COUNT>/k_scan/k_bin<EMIT_PACKED>   the same with exact packing (large workloads).
-//   k_sort             one workgroup per tile: LDS LSD radix sort of the bucket on the varying depth bits (wave
-//                      ballot multisplit ranks, per-wave chunks => stable), ties ordered by Gaussian id. The result
-//                      is exactly upstream's order: its LSD sort is stable on index-ordered pairs, so equal depths
-//                      keep increasing Gaussian id. Buckets > 8192 use an in-place bitonic network on the u64
+//   k_sort             one workgroup per tile: one MSD bucket pass on the top 11 bits of the tile's depth span,
+//                      then each entry ranked inside its (small) bucket on (depth, id); clustered depths fall back
+//                      to LDS LSD radix passes (wave ballot multisplit ranks, per-wave chunks => stable). Ties are
+//                      ordered by Gaussian id, which is exactly upstream's order: its LSD sort is stable on
+//                      index-ordered pairs. Buckets > RS_CAP (4032) use an in-place bitonic network on the u64
 //                      composite key (LDS blocks + global merge stages).
 #include "render_common.h"
 
@@ -476,16 +477,21 @@ __global__ __launch_bounds__(ORD_THREADS) void k_order(int M, long long slot_str
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Per-tile sort: RS_CAP entries sorted in LDS (larger buckets take sort_oversized): u32 keys, u16 bucket positions
-// and per-wave 512-bucket counters (40 KB at 512 threads; 8 rows per lane keep it at ~90 VGPRs).
+// Per-tile sort: up to RS_CAP entries sorted in LDS (larger buckets take sort_oversized): u32 keys, u16 bucket
+// positions and per-wave 512-bucket counters; 8 rows per lane.
+// RS_CAP is 4032, not 4096: the workgroup's whole LDS (the dynamic image, RS_CAP * 8 + 8 KB on the MSD path, plus
+// ~400 B of static __shared__) must stay <= 40 KB for 4 workgroups per CU (160 KB). At 4096 it was 41,360 B and
+// the kernel ran 3 per CU; lists of 4033..4096 entries now take the (rare) oversized path.
 #ifndef LGM_RS_THREADS
 #define LGM_RS_THREADS 512
 #endif
 #ifndef LGM_RS_CAP
-#define LGM_RS_CAP 4096
+#define LGM_RS_CAP 4032
 #endif
 constexpr int RS_THREADS = LGM_RS_THREADS, RS_WAVES = RS_THREADS / 64, RS_CAP = LGM_RS_CAP,
-              RS_MAXR = RS_CAP / RS_THREADS;
+              RS_MAXR = (RS_CAP + RS_THREADS - 1) / RS_THREADS;
+constexpr int RS_OBLK = 4096;  // sort_oversized's LDS block (a power of two), u64 keys over the image
+static_assert(RS_CAP <= RS_OBLK && RS_CAP % 64 == 0, "sort image layout");
 constexpr int RS_DBITS = 9, RS_B = 1 << RS_DBITS;  // digit width: a typical 26-bit depth span takes 3 passes
 #ifndef LGM_RS_CNT16
 #define LGM_RS_CNT16 1  // per-wave digit counters as u16 (they never exceed RS_CAP): halves their LDS
@@ -495,7 +501,9 @@ typedef std::conditional<LGM_RS_CNT16, unsigned short, int>::type RsCnt;
 constexpr int RS_LDS_LSD = RS_CAP * 4 + RS_CAP * 2 + RS_WAVES * RS_B * (int)sizeof(RsCnt);
 constexpr int RS_LDS = RS_LDS_LSD > RS_CAP * 8 + 2048 * 4 ? RS_LDS_LSD : RS_CAP * 8 + 2048 * 4;
 static_assert(RS_CAP < 65536, "u16 counters");
-static_assert(RS_LDS >= RS_CAP * 8, "sort_oversized reuses the image as u64[RS_CAP]");
+static_assert(RS_LDS >= RS_OBLK * 8, "sort_oversized reuses the image as u64[RS_OBLK]");
+static_assert(RS_CAP > 4032 || RS_LDS + 512 <= 160 * 1024 / 4,  // (larger caps only for A/B timing)
+              "4 sort workgroups per CU (with the static __shared__ words)");
 static_assert(RS_B % RS_THREADS == 0 || RS_THREADS % RS_B == 0, "bucket scan layout");
 
 __device__ __forceinline__ unsigned long long lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
@@ -594,10 +602,10 @@ __device__ __forceinline__ void cas64(unsigned long long *s, int lo, int hi) {
 }
 
 // Buckets larger than RS_CAP: bitonic network ("flip + half-cleaner" form, all comparators ascending, entries at
-// index >= n act as +inf) on the u64 composite keys in place: LDS blocks of RS_CAP for short distances, global
+// index >= n act as +inf) on the u64 composite keys in place: LDS blocks of RS_OBLK for short distances, global
 // memory for long ones. Rare (only huge central tiles); correct for any n.
 __device__ void sort_oversized(unsigned long long *seg, int n, unsigned long long *sk) {
-    const int C = RS_CAP;
+    const int C = RS_OBLK;
     int m = 1;
     while (m < n) m <<= 1;
     for (int c0 = 0; c0 < n; c0 += C) {  // sort each LDS block
@@ -673,6 +681,9 @@ __device__ void sort_oversized(unsigned long long *seg, int n, unsigned long lon
 #ifndef LGM_SORT_MSD
 #define LGM_SORT_MSD 1
 #endif
+#ifndef LGM_SORT_KV
+#define LGM_SORT_KV 1
+#endif
 constexpr int MSD_BITS = 11, MSD_B = 1 << MSD_BITS, MSD_LIMIT = 48;
 static_assert(MSD_B % RS_THREADS == 0, "scan layout");
 
@@ -711,6 +722,29 @@ __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const un
     }
     __syncthreads();
     // scatter (arbitrary order inside a bucket); afterwards hc[b] is the END of bucket b (= start of b + 1)
+#if LGM_SORT_KV
+    // key and id side by side (the sk / si image read as one u64 array): one 8-B LDS write per entry here and one
+    // 8-B read per bucket entry in the ranking, on the composite (key << 32 | id) order
+    unsigned long long *skv = reinterpret_cast<unsigned long long *>(sk);
+#pragma unroll
+    for (int r = 0; r < RS_MAXR; r++) {
+        const int e = c0 + r * 64 + lane;
+        if (r < R && e < n) {
+            const unsigned pos = atomicAdd(&hc[kr[r] >> shift], 1u);
+            skv[pos] = ((unsigned long long)kr[r] << 32) | ir[r];
+        }
+    }
+    __syncthreads();
+    for (int q = tid; q < n; q += RS_THREADS) {
+        const unsigned long long cq = skv[q];
+        const unsigned bq = (unsigned)(cq >> 32) >> shift;
+        const int lo = bq ? (int)hc[bq - 1] : 0, hi = (int)hc[bq];
+        int rank = lo;
+        for (int z = lo; z < hi; z++) rank += skv[z] < cq ? 1 : 0;
+        ids_out[rank] = (unsigned)cq;
+    }
+    return true;
+#endif
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         const int e = c0 + r * 64 + lane;

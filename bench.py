@@ -59,17 +59,25 @@ def kernel_bytes(N, BV, K, P, B=None):
     }
 
 
-def limiter_from_counters(rec, achieved_counter_gbs):
+N_SIMD, CLK_HZ = 256 * 4, 2.4e9  # MI355X: 256 CUs x 4 SIMDs; peak engine clock
+
+
+def limiter_from_counters(rec, achieved_counter_gbs, avg_s=None):
     """What bounds a kernel, read off its PMC record (profiles/pmc_latest.json): HBM if the counted traffic runs at
-    >= 60 % of peak, VALU if the VALU pipe is busy >= 60 % of the wave cycles, else latency / issue (the waves wait)."""
+    >= 60 % of peak; VALU issue if its VALU instructions fill >= 70 % of the chip's SIMD issue cycles over the
+    launch (a wave64 VALU instruction takes 2 cycles on CDNA4's 32-wide SIMDs; counted at the peak clock, so a lower
+    bound); else latency / issue (the waves wait: barriers, LDS and memory round trips)."""
     if not rec:
         return None
     hbm = achieved_counter_gbs / PEAK_HBM_GBS if achieved_counter_gbs else 0.0
     valu, wait = rec.get("valu_busy_frac", 0.0), rec.get("wait_frac", 0.0)
     lds = rec.get("lds_bank_conflict_frac")
-    kind = "hbm" if hbm >= 0.6 else "valu" if valu >= 0.6 else "latency/issue"
-    return {"kind": kind, "hbm_frac_at_counter_bytes": round(hbm, 4), "valu_busy_frac": valu, "wait_frac": wait,
-            "lds_bank_conflict_frac": lds}
+    issue = None
+    if avg_s and rec.get("SQ_INSTS_VALU"):
+        issue = round(2.0 * rec["SQ_INSTS_VALU"] / (N_SIMD * avg_s * CLK_HZ), 4)
+    kind = "hbm" if hbm >= 0.6 else "valu-issue" if (issue or 0.0) >= 0.7 else "latency/issue"
+    return {"kind": kind, "hbm_frac_at_counter_bytes": round(hbm, 4), "valu_issue_frac": issue,
+            "valu_busy_frac_per_wave": valu, "wait_frac": wait, "lds_bank_conflict_frac": lds}
 
 
 def pmc_record(kernel):
@@ -538,7 +546,7 @@ def run(args):
                               "bytes_per_launch": kb.get(dom, 0),
                               "frac_at_binned_K": round(binned / PEAK_HBM_GBS, 4),
                               "frac_at_counter_bytes": round(counter_gbs / PEAK_HBM_GBS, 4) if counter_gbs else None,
-                              "limiter": limiter_from_counters(json_pmc(dom), counter_gbs),
+                              "limiter": limiter_from_counters(json_pmc(dom), counter_gbs, dom_avg_s),
                               **pmc}
         result["kernel_rooflines"] = {
             k: {"avg_us": round(1e3 * ms / n, 2), "bytes": kb.get(k), "frac": round(kb[k] / (ms / n / 1e3) / 1e9 /

@@ -97,6 +97,9 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #define LGM_BWD_FLUSH_WAVES 0  // 1: the gradient atomics on waves 1-3 only, the staging wait on wave 0 only
                                // (measured slower: 622 -> 694 us on the pool, profiles/r03/ab_bwd_flush)
 #endif
+#ifndef LGM_BWD_SPLIT3
+#define LGM_BWD_SPLIT3 2  // moment MFMA operand split: 0 two-term, 1 three-term, 2 three-term in deterministic mode
+#endif
 #ifndef LGM_BWD_CHUNK
 #define LGM_BWD_CHUNK 64  // backward entries per staged chunk (the per-wave moment slots scale with it)
 #endif
@@ -873,6 +876,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     int myj = 0;  // the chunk row of this lane's batch column (ql & 7)
+    // Moment precision: the two-term split carries ~2^-16 per product; the three-term split makes the products
+    // exact (+2 MFMAs and +40 VALU per 8-entry batch: k_render_bwd +7 % on the pool). On needle-like footprints (conic
+    // condition > ~1e3) the cov2D inverse amplifies that 2^-16 into their scale / rotation gradients: at 512^2 the
+    // two-term kernel sits at ~2x the fp32 oracle's own error vs fp64 in mean / scale / rot, the three-term one
+    // below it (profiles/r03/diag_float_spread). The deterministic mode -- the reproducible, precise setting --
+    // takes the three-term split; the float default keeps the two-term one.
+    constexpr bool SPLIT3 = LGM_BWD_SPLIT3 == 1 || (LGM_BWD_SPLIT3 == 2 && DET);
     // B operand of the current batch: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t)
     auto read_batch = [&](float (&xs)[2][8]) {
 #pragma unroll
@@ -886,6 +896,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // split hi + lo, the moment MFMAs, and the lane's (at most 4) live results into this wave's slots
     auto mfma_batch = [&](const float (&xs)[2][8], int col) {
         f32x4 a2[2];
+        if (SPLIT3) {
+#pragma unroll
+        for (int t2 = 0; t2 < 2; t2++) {
+            // hi = the top 16 bits, mid = the top 16 bits of the (exact) remainder, lo = what is left (<= 8
+            // significant bits: exact in bf16): hi + mid + lo = x, so the geometric moments (A exact in bf16) are
+            // fp32 accumulations of exact products
+            bf16x8 bh, bm, bl;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const unsigned ub = __builtin_bit_cast(unsigned, xs[t2][j]);
+                bh[j] = __builtin_bit_cast(__bf16, (unsigned short)(ub >> 16));
+                const float r1 = xs[t2][j] - __builtin_bit_cast(float, ub & 0xffff0000u);
+                const unsigned ur = __builtin_bit_cast(unsigned, r1);
+                bm[j] = __builtin_bit_cast(__bf16, (unsigned short)(ur >> 16));
+                bl[j] = (__bf16)(r1 - __builtin_bit_cast(float, ur & 0xffff0000u));
+            }
+            f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
+            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);
+            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bm, cacc, 0, 0, 0);
+            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, cacc, 0, 0, 0);
+            a2[t2] = cacc;
+        }
+        } else {
 #pragma unroll
         for (int t2 = 0; t2 < 2; t2++) {
             bf16x8 bh, bl;
@@ -899,6 +932,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, cacc, 0, 0, 0);
             a2[t2] = cacc;
+        }
         }
         const f32x4 acc = a2[0] + a2[1];
         // D[row = 4 qk + r][col = ql]: moments 0..5 in the w columns, rows 6..9 in the u columns; each lane stores its

@@ -62,6 +62,8 @@ __device__ __forceinline__ int wave_max_i32(int v) {
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 constexpr int WU_LD = 68;  // row stride of the per-wave [16 columns][64 pixels] gradient image (16-B aligned rows)
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+typedef __attribute__((ext_vector_type(2))) float f32x2v;
 constexpr int MB = 8;      // entries per moment-MFMA batch (columns 0..7: w, 8..15: u)
 
 // One staged 256-entry chunk, written by LDS DMA (global_load_lds: 16-B lane stride for both the 16-B and the
@@ -97,8 +99,11 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #define LGM_BWD_FLUSH_WAVES 0  // 1: the gradient atomics on waves 1-3 only, the staging wait on wave 0 only
                                // (measured slower: 622 -> 694 us on the pool, profiles/r03/ab_bwd_flush)
 #endif
+#ifndef LGM_BWD_SPLIT_RN
+#define LGM_BWD_SPLIT_RN 1  // two-term split: round-to-nearest hi (1) or truncated hi (0)
+#endif
 #ifndef LGM_BWD_SPLIT3
-#define LGM_BWD_SPLIT3 2  // moment MFMA operand split: 0 two-term, 1 three-term, 2 three-term in deterministic mode
+#define LGM_BWD_SPLIT3 0  // moment MFMA operand split: 0 two-term, 1 three-term, 2 three-term in deterministic mode
 #endif
 #ifndef LGM_BWD_CHUNK
 #define LGM_BWD_CHUNK 64  // backward entries per staged chunk (the per-wave moment slots scale with it)
@@ -876,12 +881,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     int myj = 0;  // the chunk row of this lane's batch column (ql & 7)
-    // Moment precision: the two-term split carries ~2^-16 per product; the three-term split makes the products
-    // exact (+2 MFMAs and +40 VALU per 8-entry batch: k_render_bwd +7 % on the pool). On needle-like footprints (conic
-    // condition > ~1e3) the cov2D inverse amplifies that 2^-16 into their scale / rotation gradients: at 512^2 the
-    // two-term kernel sits at ~2x the fp32 oracle's own error vs fp64 in mean / scale / rot, the three-term one
-    // below it (profiles/r03/diag_float_spread). The deterministic mode -- the reproducible, precise setting --
-    // takes the three-term split; the float default keeps the two-term one.
+    // Moment precision. On needle-like footprints (conic condition > ~1e3) the cov2D inverse amplifies any rounding
+    // of the conic gradients into their scale / rotation gradients. A two-term split with a TRUNCATED hi part biases
+    // every product's rounding one way (~2^-16, coherent over a tile's pixels): at 512^2 it left mean / scale / rot
+    // at ~2x the fp32 oracle's own error vs fp64. Round-to-nearest hi (LGM_BWD_SPLIT_RN, same instruction count:
+    // <= 2^-17 per product, unbiased) and the exact three-term split (+2 MFMAs and +40 VALU per 8-entry batch,
+    // k_render_bwd +7 % on the pool) both put them at 0.5-0.8x the oracle's (profiles/r03/diag_float_spread), so
+    // the two-term round-to-nearest split is the default in both modes.
     constexpr bool SPLIT3 = LGM_BWD_SPLIT3 == 1 || (LGM_BWD_SPLIT3 == 2 && DET);
     // B operand of the current batch: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t)
     auto read_batch = [&](float (&xs)[2][8]) {
@@ -922,12 +928,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #pragma unroll
         for (int t2 = 0; t2 < 2; t2++) {
             bf16x8 bh, bl;
+#if LGM_BWD_SPLIT_RN
+            // hi = x rounded to bf16 (|x - hi| <= 2^-9 |x|), lo = the exact remainder rounded: <= 2^-17 |x| per
+            // product, half the truncated split's bound at the same instruction count (per pair: two packed
+            // conversions, the two hi halves back to fp32 by a shift and a mask, two subtractions)
 #pragma unroll
-            for (int j = 0; j < 8; j++) {  // hi = the top 16 bits (exact), lo = the rest rounded: ~2^-17 relative
+            for (int j = 0; j < 8; j += 2) {
+                const bf16x2v hp = __builtin_convertvector((f32x2v){xs[t2][j], xs[t2][j + 1]}, bf16x2v);
+                const unsigned hb = __builtin_bit_cast(unsigned, hp);
+                const float h0 = __builtin_bit_cast(float, hb << 16), h1 = __builtin_bit_cast(float, hb & 0xffff0000u);
+                const bf16x2v lp = __builtin_convertvector((f32x2v){xs[t2][j] - h0, xs[t2][j + 1] - h1}, bf16x2v);
+                bh[j] = hp[0];
+                bh[j + 1] = hp[1];
+                bl[j] = lp[0];
+                bl[j + 1] = lp[1];
+            }
+#else
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                // hi = the top 16 bits (exact truncation), lo = the rest rounded: <= 2^-16 |x| per product
                 const unsigned ub = __builtin_bit_cast(unsigned, xs[t2][j]);
                 bh[j] = __builtin_bit_cast(__bf16, (unsigned short)(ub >> 16));
                 bl[j] = (__bf16)(xs[t2][j] - __builtin_bit_cast(float, ub & 0xffff0000u));
             }
+#endif
             f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, cacc, 0, 0, 0);
@@ -1048,8 +1072,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                     const float lp = fmaf(Q.x * dy, dy, fmaf(fmaf(Pj.w, dy, Pj.z * dx), dx, Q.y));  // as k_render_fwd
                     const float e = __builtin_amdgcn_exp2f(lp);  // opacity G
                     const bool ok = before_last && lp <= Q.y && e >= 1.0f / 255.0f;
-                    al[u] = ok ? alpha_cap(e) : 0.f;
                     Gw[u] = ok ? e : 0.f;  // dL/dG = opacity dL/dalpha (0: the entry adds nothing here)
+                    al[u] = alpha_cap(Gw[u]);  // (= ok ? alpha_cap(e) : 0, one select less: alpha_cap(0) = 0)
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {  // the prefix recurrences in list order

@@ -295,19 +295,21 @@ def test_deterministic_backward(cuda, oracle_mod):
     _check(oracle_mod, out, g, cv, cvp, 256, 256, bg, d_m, d_alpha, name="cfg3 bench inputs (deterministic mode)")
 
 
-def test_deterministic_needles_512_at_or_below_fp32_oracle(cuda, oracle_mod):
-    """The deterministic mode's backward sums the pixel moments from a three-term bf16 split (exact products,
-    LGM_BWD_SPLIT3): on cfg4's 512^2 (153,600 Gaussians, 5 of the 20 views), whose mean / scale / rotation gradient
-    errors are carried by a few needle-like footprints (conic condition 1e3-2e4: the cov2D inverse amplifies any
-    rounding of their conic gradients), its error vs fp64 is at or below the fp32 oracle's own in those groups
-    (profiles/r03/diag_float_spread; the float default's two-term split sits near 2x there)."""
+@pytest.mark.parametrize("det", [True, False])
+def test_needles_512_vs_fp32_oracle(cuda, oracle_mod, det):
+    """cfg4's 512^2 (153,600 Gaussians, 5 of the 20 views), whose mean / scale / rotation gradient errors are carried
+    by a few needle-like footprints (conic condition 1e3-2e4: the cov2D inverse amplifies any rounding of their conic
+    gradients). The backward's moment MFMAs split w / u into round-to-nearest bf16 hi + lo parts (unbiased, <= 2^-17
+    per product; the truncated split sat near 2x the oracle's error here, profiles/r03/diag_float_spread):
+    deterministic mode at or below the fp32 oracle's own error vs fp64 in those groups; float atomics (an
+    accumulation-order draw) within the usual bar."""
     g = synthetic_gaussians(1, 153_600, seed=4)
     cv, cvp, _ = orbit_cameras(20)
     cv, cvp = cv[None, 0:20:4].contiguous(), cvp[None, 0:20:4].contiguous()
     V = cv.shape[1]
     d_img, _, d_alpha, bg = synthetic_upstream_grads(1, V, 512, 512, seed=45)
     d_m, keep = _clamp_masked_grads(oracle_mod, g, cv, cvp, 512, 512, bg, d_img)
-    os.environ["LGM_AMD_DETERMINISTIC"] = "1"
+    os.environ["LGM_AMD_DETERMINISTIC"] = "1" if det else "0"
     try:
         out = _production(cuda, g, cv, cvp, 512, 512, bg, d_img, d_alpha, keep)
     finally:
@@ -320,9 +322,10 @@ def test_deterministic_needles_512_at_or_below_fp32_oracle(cuda, oracle_mod):
     for grp, sl in GROUPS.items():
         e_gpu = rel_l2(out["d_gaussians"][..., sl], truth[..., sl])
         e_o32 = rel_l2(ref["d_gaussians"][..., sl], truth[..., sl])
-        rec[grp] = {"gpu": e_gpu, "fp32_oracle": e_o32, "bar": e_o32 if grp in ("mean", "scale", "rot")
+        rec[grp] = {"gpu": e_gpu, "fp32_oracle": e_o32, "bar": e_o32 if det and grp in ("mean", "scale", "rot")
                     else max(BWD_TOL, 2.0 * e_o32)}
-    PRECISION.append({"test": "cfg4 512^2, 5 views, needle-dominated (deterministic mode)", "groups": rec})
+    PRECISION.append({"test": f"cfg4 512^2, 5 views, needle-dominated ({'deterministic' if det else 'float'} mode)",
+                      "groups": rec})
     for grp, r in rec.items():
         assert r["gpu"] <= r["bar"], f"d_{grp}: GPU vs fp64 {r['gpu']:.3e}, fp32 oracle {r['fp32_oracle']:.3e}"
 

@@ -211,12 +211,19 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         if (MODE != COUNT) {
             const size_t k = (size_t)bv * d.N + i;
             if (vis) {
-                gP[k] = rec_p(o.x, o.y, o.A, o.B);  // pre-scaled compositing records (render_common.h)
-                gQ[k] = rec_q(o.C, o.opacity, o.tau, o.depth);
-                rects[k] = make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16), (unsigned)o.x1 | ((unsigned)o.y1 << 16));
+                const float4 rp = rec_p(o.x, o.y, o.A, o.B), rq = rec_q(o.C, o.opacity, o.tau, o.depth);
+                gP[k] = rp;  // pre-scaled compositing records (render_common.h)
+                gQ[k] = rq;
+                const bool side = ACC_SIDE && !(d.options & LGM_RENDER_DETERMINISTIC) && rec_needle(rp.z, rp.w, rq.x);
+                rects[k] = make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16),
+                                      (unsigned)o.x1 | ((unsigned)o.y1 << 16) | (side ? 0x80000000u : 0u));
+                if (side) {  // the record's fp64 conic accumulators (acc_side_offset)
+                    double *sd = reinterpret_cast<double *>(accum + acc_side_offset(d.B, d.V, d.N)) + k * 3;
+                    sd[0] = 0.0; sd[1] = 0.0; sd[2] = 0.0;
+                }
                 // the backward's per-view gradient accumulators start at zero (a repeated backward clears them with
                 // LGM_RENDER_BACKWARD_AGAIN); int64 fixed point in deterministic mode
-                if (d.options & LGM_RENDER_DETERMINISTIC) {
+                if (LGM_ACC_F64 || (d.options & LGM_RENDER_DETERMINISTIC)) {  // 8-B elements (int64 / fp64)
                     ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(accum) + k * (NACC_V / 2);
 #pragma unroll
                     for (int q = 0; q < NACC_V / 2; q++) a2[q] = make_ulonglong2(0ull, 0ull);
@@ -233,7 +240,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
             if (radii_out) radii_out[k] = vis ? o.radius : 0;
             if (bv % d.V == 0) {  // the scene's view-independent record (opacity, colour), once per scene
                 const size_t ks = (size_t)d.BV * d.N * NACC_V + ((size_t)b * d.N + i) * NACC_S;
-                if (d.options & LGM_RENDER_DETERMINISTIC) {
+                if (LGM_ACC_F64 || (d.options & LGM_RENDER_DETERMINISTIC)) {  // 8-B elements (int64 / fp64)
                     ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(reinterpret_cast<unsigned long long *>(accum) + ks);
                     a2[0] = make_ulonglong2(0ull, 0ull);
                     a2[1] = make_ulonglong2(0ull, 0ull);

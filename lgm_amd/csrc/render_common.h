@@ -23,7 +23,13 @@ constexpr int NACC_V = 6, NACC_S = 4;
 __host__ __device__ __forceinline__ size_t acc_index(int q, size_t bvN_i, size_t bN_i, size_t BVN) {
     return q < 5 ? bvN_i * NACC_V + q : q < 9 ? BVN * NACC_V + bN_i * NACC_S + (q - 5) : bvN_i * NACC_V + 5;
 }
-inline size_t acc_elems(size_t B, size_t V, size_t N) { return B * V * N * NACC_V + B * N * NACC_S; }
+__host__ __device__ inline size_t acc_elems(size_t B, size_t V, size_t N) { return B * V * N * NACC_V + B * N * NACC_S; }
+// Float mode, LGM_ACC_SIDE: the conic partials (q = 2..4) of NEEDLE records go to fp64 side accumulators, 3 per
+// (view, Gaussian), placed after the fp32 ones (float offset acc_side_offset, 8-B aligned). A needle is a record
+// whose conic condition (A + C)^2 / (AC - B^2) exceeds LGM_ACC_NEEDLE (or is not positive definite), decided on the
+// stored record (rec_needle) identically by the binning, the backward's flush and the preprocess backward (via a
+// flag in bit 31 of the record's rect).
+__host__ __device__ inline size_t acc_side_offset(size_t B, size_t V, size_t N) { return (acc_elems(B, V, N) + 1) & ~(size_t)1; }
 constexpr int LDS_HIST_MAX = 8192;                   // tiles per view for the LDS-histogram binning path
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -34,6 +40,21 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // quota stay inside the previous item. Default 0: one backward item per tile -- in this mode the split costs more
 // than its load balance returns, measured on the pool (profiles/r03/ab_det):
 // deterministic k_render_bwd 1950 / 1306 / 955 / 787 / 685 / 650 us at quota 16 / 8 / 4 / 2 / 1 / 0 (float mode 626).
+// Float mode's gradient accumulators: fp32, with fp64 for the conic partials of needle-like records. A needle-like footprint's conic partials from different
+// tiles and views largely cancel, and the cov2D inverse amplifies what is left (conditions 1e3-2e4), so fp32 atomic
+// sums made its scale / rotation gradients a draw of the atomic order (single runs up to ~3x the fp32 oracle's error
+// vs fp64 at 512^2, profiles/r03/diag_float_spread); fp64 sums of the same fp32 partials are order-independent to
+// ~2^-50 of the partials, as the deterministic mode's int64 sums are exact.
+#ifndef LGM_ACC_F64
+#define LGM_ACC_F64 0  // every float-mode accumulator fp64 (measured +37 us on the pool; LGM_ACC_SIDE instead)
+#endif
+#ifndef LGM_ACC_SIDE
+#define LGM_ACC_SIDE 1  // fp64 side accumulators for the conic partials of needle-like records only
+#endif
+#ifndef LGM_ACC_NEEDLE
+#define LGM_ACC_NEEDLE 300.0f
+#endif
+constexpr bool ACC_SIDE = LGM_ACC_SIDE && !LGM_ACC_F64;
 #ifndef LGM_CK_QUOTA
 #define LGM_CK_QUOTA 0
 #endif
@@ -83,7 +104,8 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.cklist = take((size_t)L.ck_slots * 8);
     L.nck = take(BV * T * 4);
     L.cmask = take(BV * P);
-    L.accum = take(acc_elems(B, V, N) * (det ? 8 : 4));
+    L.accum = take((det || LGM_ACC_F64) ? acc_elems(B, V, N) * 8
+                                       : acc_side_offset(B, V, N) * 4 + (ACC_SIDE ? BV * N * 3 * 8 : 0));
     L.lossp = take(BV * T * 2 * 4);  // per-tile sums of squared image / alpha residuals (fused loss)
     L.lossw = take(((BV * T + 2047) / 2048) * 16);  // their per-workgroup double2 partials (k_loss_reduce)
     L.detmax = take(64 * 4);  // deterministic mode: max |dL/dpixel| over the seeds, in 64 atomicMax slots
@@ -234,6 +256,12 @@ __device__ __forceinline__ float4 rec_p(float x, float y, float A, float B) {
 }
 __device__ __forceinline__ float4 rec_q(float C, float opacity, float tau, float depth) {
     return make_float4(-KQ * C, opacity > 0.f ? log2f(opacity) : -INFINITY, tau >= 3.0e38f ? tau : KQ * tau, depth);
+}
+// Needle-like record (see acc_side_offset): on the stored pre-scaled conic A', B', C' (the condition is
+// scale-invariant: (A' + C')^2 / (A'C' - B'^2 / 4) = (A + C)^2 / (AC - B^2)).
+__device__ __forceinline__ bool rec_needle(float Ap, float Bp, float Cp) {
+    const float sac = Ap + Cp, dq = Ap * Cp - 0.25f * Bp * Bp;
+    return !(sac * sac <= LGM_ACC_NEEDLE * dq);  // (dq <= 0 or NaN: flagged)
 }
 __device__ __forceinline__ bool rec_hits_rect(const float4 &p, const float4 &q, float rx0, float rx1, float ry0,
                                               float ry1) {

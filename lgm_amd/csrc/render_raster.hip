@@ -741,6 +741,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     constexpr int NC = DEPTH ? 4 : 3, NROW = 6 + 2 * NC;
     __shared__ __attribute__((aligned(16))) float sAccW[4][LS * (NROW + 1)];
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
+    __shared__ int s_ndl;  // the chunk holds a needle-like record (ACC_SIDE)
+
     // ---- work item: (tile, chunk c, checkpoint slot)
     const int M = d.BV * d.T, Mp = LGM_XCD_ORDER ? round8(M) : M;  // head items, then the checkpoint items
     int tile, c = 0, slot = -1;
@@ -1000,6 +1002,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         // one row per lane: every wave tests all CH entries against its OWN quadrant (one ellipse test per lane
         // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
         if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
+        if (ACC_SIDE && !DET && tid == 0) s_ndl = 0;  // (published by the barrier after the quadrant tests)
         {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
             static_assert((4 * LS * (NROW + 1)) % 4 == 0, "slot zeroing by float4");
             float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
@@ -1156,6 +1159,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #pragma unroll
                 for (int qq = 0; qq < NV; qq++) part[qq] = ldexpf(part[qq], det_s + (qq < 5 ? nm.k[qq] : 0));
             }
+            if (ACC_SIDE && !DET) {  // a needle's conic partials move to the (dead) lo rows NV.. for the fp64 flush
+                const bool ndl = rec_needle(Pj.z, Pj.w, Qj.x);
+#pragma unroll
+                for (int qq = 2; qq <= 4; qq++) {
+                    o[(NV + qq - 2) * LS + j] = ndl ? part[qq] : 0.f;
+                    part[qq] = ndl ? 0.f : part[qq];
+                }
+                if (ndl) s_ndl = 1;  // (benign race: every writer stores 1)
+            }
 #pragma unroll
             for (int qq = 0; qq < NV; qq++) o[qq * LS + j] = part[qq];
         }
@@ -1181,7 +1193,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
                 const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
 #ifdef LGM_TIMING_NO_ATOMICS  // timing-only build: the flush's atomics become plain stores of the same shape
-                if (a != 0.f) accum[ai] = a;
+                if (a != 0.f) {
+                    if (LGM_ACC_F64) reinterpret_cast<double *>(accum)[ai] = a;
+                    else accum[ai] = a;
+                }
                 if (false) {
 #else
                 if (a != 0.f) {
@@ -1189,8 +1204,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                     if (DET)  // integer adds commute: order-independent sums (a is already in fixed-point units)
                         atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
                                   (unsigned long long)__float2ll_rn(fminf(fmaxf(a, -9.0e18f), 9.0e18f)));
+                    else if (LGM_ACC_F64)  // (global_atomic_add_f64)
+                        atomicAdd(reinterpret_cast<double *>(accum) + ai, (double)a);
                     else
                         atomicAdd(accum + ai, a);
+                }
+            }
+        }
+        if (ACC_SIDE && !DET && s_ndl) {  // (workgroup-uniform) the chunk's needle conic partials, fp64
+            int tt = tid;
+            asm volatile("" : "+v"(tt));  // (recomputed here: lane indices hoisted out of the chunk loop spilled)
+            if (tt < 3 * CH) {
+                const int j = tt % CH, c3 = tt / CH;
+                const float a = sAccW[0][(NV + c3) * LS + j];
+                if (a != 0.f && b0 + j < s1) {
+                    const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
+                    // (the side block's offset recomputed here from the SGPR dims: a pointer hoisted out of the
+                    // chunk loop was kept in VGPRs and spilled)
+                    const size_t so = acc_side_offset(d.B, d.V, d.N) / 2;
+                    atomicAdd(reinterpret_cast<double *>(accum) + so + (gbase + gid) * 3 + c3, (double)a);
                 }
             }
         }
@@ -1302,6 +1334,14 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
                 acc[2 * q] = (float)ldexp((double)a.x, -(det_s + nm.k[2 * q]));
                 acc[2 * q + 1] = (float)ldexp((double)a.y, -(det_s + nm.k[2 * q + 1]));
             }
+        } else if (LGM_ACC_F64) {
+            const double2 *acc2 = reinterpret_cast<const double2 *>(accum) + k * (NACC_V / 2);
+#pragma unroll
+            for (int q = 0; q < NACC_V / 2; q++) {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
+                const double2 a = acc2[q];
+                acc[2 * q] = (float)a.x;
+                acc[2 * q + 1] = (float)a.y;
+            }
         } else {
             const float2 *acc2 = reinterpret_cast<const float2 *>(accum + k * NACC_V);
 #pragma unroll
@@ -1310,6 +1350,12 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
                 acc[2 * q] = a.x;
                 acc[2 * q + 1] = a.y;
             }
+        }
+        if (ACC_SIDE && !det && (r.y >> 31)) {  // a needle: its conic partials were summed in fp64
+            const double *sd = reinterpret_cast<const double *>(accum + acc_side_offset(d.B, d.V, d.N)) + k * 3;
+            acc[2] = (float)sd[0];
+            acc[3] = (float)sd[1];
+            acc[4] = (float)sd[2];
         }
         const float dm2x = acc[0], dm2y = acc[1];
         const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
@@ -1392,6 +1438,11 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
             dop = (float)ldexp((double)a[0], -det_s);
 #pragma unroll
             for (int q = 0; q < 3; q++) dcol[q] = (float)ldexp((double)a[1 + q], -det_s);
+        } else if (LGM_ACC_F64) {
+            const double2 *a = reinterpret_cast<const double2 *>(reinterpret_cast<const double *>(accum) + ks);
+            const double2 a0 = a[0], a1 = a[1];
+            dop = (float)a0.x;
+            dcol[0] = (float)a0.y; dcol[1] = (float)a1.x; dcol[2] = (float)a1.y;
         } else {
             const float4 a = *reinterpret_cast<const float4 *>(accum + ks);
             dop = a.x;
@@ -1466,7 +1517,9 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
     // the per-view accumulators were zeroed by the forward's binning; a repeated backward of the same forward
     // clears what the previous one left
     if ((d.options & LGM_RENDER_BACKWARD_AGAIN) &&
-        hipMemsetAsync(ws + L.accum, 0, acc_elems(d.B, d.V, d.N) * ((d.options & LGM_RENDER_DETERMINISTIC) ? 8 : 4),
+        hipMemsetAsync(ws + L.accum, 0, (LGM_ACC_F64 || (d.options & LGM_RENDER_DETERMINISTIC))
+                                            ? acc_elems(d.B, d.V, d.N) * 8
+                                            : acc_side_offset(d.B, d.V, d.N) * 4 + (ACC_SIDE ? (size_t)d.BV * d.N * 24 : 0),
                        st) != hipSuccess) {
         set_error("hipMemsetAsync failed");
         return LGM_E_HIP;

@@ -40,13 +40,14 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // quota stay inside the previous item. Default 0: one backward item per tile -- in this mode the split costs more
 // than its load balance returns, measured on the pool (profiles/r03/ab_det):
 // deterministic k_render_bwd 1950 / 1306 / 955 / 787 / 685 / 650 us at quota 16 / 8 / 4 / 2 / 1 / 0 (float mode 626).
-// Float mode's gradient accumulators: fp32, with fp64 for the conic partials of needle-like records. A needle-like footprint's conic partials from different
-// tiles and views largely cancel, and the cov2D inverse amplifies what is left (conditions 1e3-2e4), so fp32 atomic
-// sums made its scale / rotation gradients a draw of the atomic order (single runs up to ~3x the fp32 oracle's error
-// vs fp64 at 512^2, profiles/r03/diag_float_spread); fp64 sums of the same fp32 partials are order-independent to
-// ~2^-50 of the partials, as the deterministic mode's int64 sums are exact.
+// Float mode's gradient accumulators: fp32, and fp64 for the conic partials of needle-like records. A needle's conic
+// partials from different tiles and views largely cancel and the cov2D inverse amplifies what is left (conditions
+// 1e3-2e4), so fp32 atomic sums made its scale / rotation gradients a draw of the atomic order (single runs up to ~3x
+// the fp32 oracle's error vs fp64 at 512^2, profiles/r03/diag_float_spread); fp64 sums of the same fp32 partials are
+// order-independent to ~2^-50 of the partials (the deterministic mode's int64 sums are exact). Measured: all
+// accumulators fp64 +37 us per pool step, the needle side accumulators +24 us (profiles/r03/ab_acc_side).
 #ifndef LGM_ACC_F64
-#define LGM_ACC_F64 0  // every float-mode accumulator fp64 (measured +37 us on the pool; LGM_ACC_SIDE instead)
+#define LGM_ACC_F64 0  // every float-mode accumulator fp64
 #endif
 #ifndef LGM_ACC_SIDE
 #define LGM_ACC_SIDE 1  // fp64 side accumulators for the conic partials of needle-like records only

@@ -269,6 +269,11 @@ def test_exact_count_path_matches_slot_path_512(cuda, monkeypatch):
         rec[grp] = {"float_packed_vs_float_slot": rel_l2(fl["d_gaussians"][..., sl], fl2["d_gaussians"][..., sl]),
                     "float_vs_deterministic": rel_l2(fl2["d_gaussians"][..., sl], slot["d_gaussians"][..., sl])}
     PRECISION.append({"test": "cfg4 512^2, 5 views: float-atomic accumulation-order spread", "groups": rec})
+    # with the fp64 side accumulators for needle-like records the default float path sits at the flat 1e-4 bar
+    # (measured r03/s5: rot 5.5e-6 packed vs slot, 6.1e-5 vs deterministic; round 2 had 8.5e-4)
+    for grp, r in rec.items():
+        for k, v in r.items():
+            assert v <= BWD_TOL, f"d_{grp} {k}: {v:.3e} > {BWD_TOL:.0e}"
 
 
 def test_deterministic_backward(cuda, oracle_mod):

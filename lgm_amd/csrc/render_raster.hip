@@ -99,6 +99,9 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #define LGM_BWD_FLUSH_WAVES 0  // 1: the gradient atomics on waves 1-3 only, the staging wait on wave 0 only
                                // (measured slower: 622 -> 694 us on the pool, profiles/r03/ab_bwd_flush)
 #endif
+#ifndef LGM_BWD_FLUSH_OPAQUE
+#define LGM_BWD_FLUSH_OPAQUE 1  // flush indices recomputed per chunk (no spilled per-lane offsets)
+#endif
 #ifndef LGM_BWD_SPLIT_RN
 #define LGM_BWD_SPLIT_RN 1  // two-term split: round-to-nearest hi (1) or truncated hi (0)
 #endif
@@ -1183,7 +1186,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
         constexpr int FT = LGM_BWD_FLUSH_WAVES ? 192 : 256;  // flushing threads
-        const int ft = LGM_BWD_FLUSH_WAVES ? tid - 64 : tid;
+        int ftid = tid;
+#if LGM_BWD_FLUSH_OPAQUE
+        // the lane's (entry, partial) indices recomputed per chunk: hoisted out of the chunk loop, their 64-bit
+        // per-scene accumulator offsets were spilled, and each reload's vmcnt(0) waited for this flush's earlier atomics
+        asm volatile("" : "+v"(ftid));
+#endif
+        const int ft = LGM_BWD_FLUSH_WAVES ? ftid - 64 : ftid;
 #pragma unroll
         for (int it = 0; it < (CH * NACC + FT - 1) / FT; it++) {
             const int f = it * FT + ft;

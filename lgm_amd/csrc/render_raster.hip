@@ -99,6 +99,9 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #define LGM_BWD_FLUSH_WAVES 0  // 1: the gradient atomics on waves 1-3 only, the staging wait on wave 0 only
                                // (measured slower: 622 -> 694 us on the pool, profiles/r03/ab_bwd_flush)
 #endif
+#ifndef LGM_FWD_CK_OPAQUE
+#define LGM_FWD_CK_OPAQUE 1  // forward checkpoint addresses recomputed per chunk (no spilled lane pointer)
+#endif
 #ifndef LGM_BWD_FLUSH_OPAQUE
 #define LGM_BWD_FLUSH_OPAQUE 1  // flush indices recomputed per chunk (no spilled per-lane offsets)
 #endif
@@ -322,12 +325,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         if (c >= 1) {
             const int sl = s_ck[c & 1];  // workgroup-uniform
             if (sl >= 0) {
-                float *cp = ck + (size_t)sl * 5 * TILE_PIX;
-                cp[tid] = fabsf(Tr);
-                cp[TILE_PIX + tid] = C0;
-                cp[2 * TILE_PIX + tid] = C1;
-                cp[3 * TILE_PIX + tid] = C2;
-                cp[4 * TILE_PIX + tid] = D;
+                int ctid = tid;
+#if LGM_FWD_CK_OPAQUE
+                // (the lane's checkpoint address recomputed here: hoisted out of the chunk loop, ck + tid was spilled
+                // and its reload's vmcnt(0) waited for the chunk's outstanding loads)
+                asm volatile("" : "+v"(ctid));
+#endif
+                float *cp = ck + (size_t)sl * 5 * TILE_PIX + ctid;
+                cp[0] = fabsf(Tr);
+                cp[TILE_PIX] = C0;
+                cp[2 * TILE_PIX] = C1;
+                cp[3 * TILE_PIX] = C2;
+                cp[4 * TILE_PIX] = D;
                 if (tid == 0) {
                     cklist[sl] = make_int2(tile, c);
                     ck_written = c;

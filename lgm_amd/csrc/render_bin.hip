@@ -691,6 +691,9 @@ __device__ void sort_oversized(unsigned long long *seg, int n, unsigned long lon
 #ifndef LGM_SORT_KV
 #define LGM_SORT_KV 1
 #endif
+#ifndef LGM_SORT_LOAD_ALL
+#define LGM_SORT_LOAD_ALL 1
+#endif
 constexpr int MSD_BITS = 11, MSD_B = 1 << MSD_BITS, MSD_LIMIT = 48;
 static_assert(MSD_B % RS_THREADS == 0, "scan layout");
 
@@ -796,13 +799,27 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     unsigned kr[RS_MAXR], ir[RS_MAXR];
     unsigned short pr[RS_MAXR];
     unsigned lmin = 0xffffffffu, lmax = 0u, vmax = 0u;
+#if LGM_SORT_LOAD_ALL
+    // every row's load issued before the first use (clamped index, no per-row branch around the load): with the
+    // load inside the per-row branch each row waited for its own round trip (vmcnt(0) per row, R serial trips)
+    unsigned long long xv[RS_MAXR];
+#pragma unroll
+    for (int r = 0; r < RS_MAXR; r++) {
+        const int e = c0 + r * 64 + lane;
+        if (r < R) xv[r] = seg[min(e, n - 1)];  // (r < R is workgroup-uniform)
+    }
+#endif
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         kr[r] = 0u;
         ir[r] = 0u;
         const int e = c0 + r * 64 + lane;
         if (r < R && e < n) {
+#if LGM_SORT_LOAD_ALL
+            const unsigned long long x = xv[r];
+#else
             const unsigned long long x = seg[e];
+#endif
             kr[r] = (unsigned)(x >> 32);
             ir[r] = (unsigned)x;
             lmin = min(lmin, kr[r]);

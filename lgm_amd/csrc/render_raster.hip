@@ -99,6 +99,9 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #define LGM_BWD_FLUSH_WAVES 0  // 1: the gradient atomics on waves 1-3 only, the staging wait on wave 0 only
                                // (measured slower: 622 -> 694 us on the pool, profiles/r03/ab_bwd_flush)
 #endif
+#ifndef LGM_PREPROC_ACC_EARLY
+#define LGM_PREPROC_ACC_EARLY 1  // preprocess backward: accumulator row loaded beside the rect
+#endif
 #ifndef LGM_FWD_CK_OPAQUE
 #define LGM_FWD_CK_OPAQUE 1  // forward checkpoint addresses recomputed per chunk (no spilled lane pointer)
 #endif
@@ -1336,6 +1339,16 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         const int bv = b * d.V + v;
         const size_t k = (size_t)bv * d.N + i;
         const uint2 r = rects[k];
+#if LGM_PREPROC_ACC_EARLY
+        // float mode: the accumulator row is loaded beside the rect, not after it (one memory round trip per view
+        // instead of two; an invisible view's row is uninitialised workspace, loaded and dropped)
+        float2 acc_e[NACC_V / 2];
+        if (!det && !LGM_ACC_F64) {
+            const float2 *acc2 = reinterpret_cast<const float2 *>(accum + k * NACC_V);
+#pragma unroll
+            for (int q = 0; q < NACC_V / 2; q++) acc_e[q] = acc2[q];
+        }
+#endif
         const bool vis = (r.x & 0xffff) != (r.y & 0xffff);
         if (!vis) {
             if (d_means2D) { d_means2D[2 * k] = 0.f; d_means2D[2 * k + 1] = 0.f; }
@@ -1364,7 +1377,12 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
             const float2 *acc2 = reinterpret_cast<const float2 *>(accum + k * NACC_V);
 #pragma unroll
             for (int q = 0; q < NACC_V / 2; q++) {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
+#if LGM_PREPROC_ACC_EARLY
+                const float2 a = acc_e[q];
+                (void)acc2;
+#else
                 const float2 a = acc2[q];
+#endif
                 acc[2 * q] = a.x;
                 acc[2 * q + 1] = a.y;
             }

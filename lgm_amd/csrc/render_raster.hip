@@ -102,6 +102,9 @@ using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
 #ifndef LGM_PREPROC_ACC_EARLY
 #define LGM_PREPROC_ACC_EARLY 1  // preprocess backward: accumulator row loaded beside the rect
 #endif
+#ifndef LGM_BWD_PROLOGUE_FLAT
+#define LGM_BWD_PROLOGUE_FLAT 1  // backward prologue: every per-pixel load issued before the first use
+#endif
 #ifndef LGM_FWD_CK_OPAQUE
 #define LGM_FWD_CK_OPAQUE 1  // forward checkpoint addresses recomputed per chunk (no spilled lane pointer)
 #endif
@@ -592,6 +595,13 @@ __device__ __forceinline__ void pixel_seed(const Dims &d, bool inside, int bv, s
             dp1 = di[P + pid];
             dp2 = di[2 * P + pid];
         }
+#if LGM_BWD_PROLOGUE_FLAT
+        unsigned cm = 7u;
+        float dd = 0.f, da = 0.f;
+        if (d.options & LGM_RENDER_CLAMP_IMAGE) cm = cmask[bv * P + pid];
+        if (DEPTH) dd = d_depth[bv * P + pid];
+        if (d_alpha) da = d_alpha[bv * P + pid];
+#endif
         if (LOSS) {
             // the MSE seeds (core/models.py:148): dL/dimage += 2 (image - gt) dL/dmse_image / numel, likewise alpha;
             // image recomputed from the forward's totals exactly as the forward formed it
@@ -610,6 +620,17 @@ __device__ __forceinline__ void pixel_seed(const Dims &d, bool inside, int bv, s
             dp2 += s_img * (c2 - (gi[2 * P + pid] * m + bg[2] * (1.f - m)));
             dpa = s_a * ((1 - T_final) - m);
         }
+#if LGM_BWD_PROLOGUE_FLAT
+        // (the loads are all issued above, in the blocks that only load: each use waits for the one round trip
+        // they share -- with the loads next to their uses, the clamp mask and d_alpha were two serial trips)
+        if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // torch clamp gradient: passes where 0 <= x <= 1
+            dp0 = (cm & 1u) ? dp0 : 0.f;
+            dp1 = (cm & 2u) ? dp1 : 0.f;
+            dp2 = (cm & 4u) ? dp2 : 0.f;
+        }
+        if (DEPTH) dpd = dd;
+        dpa += da;
+#else
         if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // torch clamp gradient: passes where 0 <= x <= 1
             const unsigned m = cmask[bv * P + pid];
             dp0 = (m & 1u) ? dp0 : 0.f;
@@ -618,6 +639,7 @@ __device__ __forceinline__ void pixel_seed(const Dims &d, bool inside, int bv, s
         }
         if (DEPTH) dpd = d_depth[bv * P + pid];
         if (d_alpha) dpa += d_alpha[bv * P + pid];
+#endif
     }
     o.dp0 = dp0; o.dp1 = dp1; o.dp2 = dp2; o.dpd = dpd; o.dpa = dpa;
     o.cf = cf;
@@ -802,18 +824,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const size_t pid = inside ? (size_t)d.W * py + px : 0;
     const float T_final = inside ? final_T[bv * P + pid] : 0.f;
     const int last = inside ? n_contrib[bv * P + pid] : 0;
+#if LGM_BWD_PROLOGUE_FLAT
+    // the checkpoint's loads go out before the seeds' (one shared round trip instead of a third serial one)
+    float ckT = 1.0f, ck1 = 0.f, ck2 = 0.f, ck3 = 0.f, ck4 = 0.f;
+    if (slot >= 0) {
+        const float *cp = ck + (size_t)slot * 5 * TILE_PIX;
+        ckT = cp[tid];
+        ck1 = cp[TILE_PIX + tid];
+        ck2 = cp[2 * TILE_PIX + tid];
+        ck3 = cp[3 * TILE_PIX + tid];
+        if (DEPTH) ck4 = cp[4 * TILE_PIX + tid];
+    }
+#endif
     PixelSeed sd;
     pixel_seed<DEPTH, LOSS>(d, inside, bv, P, pid, T_final, bg, cfin, d_img, d_depth, d_alpha, cmask, sd);
     const float dp0 = sd.dp0, dp1 = sd.dp1, dp2 = sd.dp2, dpd = sd.dpd, dpa = sd.dpa;
     const float4 cf = sd.cf;
     // per-pixel state entering the chunk: the forward's checkpoint (or the list head)
     float Tr = 1.0f, Dup = 0.f;
+#if LGM_BWD_PROLOGUE_FLAT
+    if (slot >= 0) {
+        Tr = ckT;
+        Dup = fmaf(ck1, dp0, fmaf(ck2, dp1, ck3 * dp2));
+        if (DEPTH) Dup = fmaf(ck4, dpd, Dup);
+    }
+#else
     if (slot >= 0) {
         const float *cp = ck + (size_t)slot * 5 * TILE_PIX;
         Tr = cp[tid];
         Dup = fmaf(cp[TILE_PIX + tid], dp0, fmaf(cp[2 * TILE_PIX + tid], dp1, cp[3 * TILE_PIX + tid] * dp2));
         if (DEPTH) Dup = fmaf(cp[4 * TILE_PIX + tid], dpd, Dup);
     }
+#endif
     init_sentinel(S);  // (published by the first barrier of the chunk loop)
     // the forward's per-wave maxima of the last contributors: positions >= wlast touch no pixel of this wave, and
     // entries behind every pixel's last contributor are never visited

@@ -202,6 +202,28 @@ def cpu_baseline_attention(seconds):
             "sample": f"attention_cpu fwd+bwd, L=4096 H=16 D=32 fp32, 1 object: {reps} repetitions in {el:.1f} s"}
 
 
+def step_spread(step, n: int) -> dict:
+    """Per-step GPU time of n more steps (an untimed pass, after the timed loop): CUDA events between consecutive
+    steps on the current stream, min / median / max in ms -- so noise of the size of a kernel-level win is visible
+    in the line next to the timed mean."""
+    import torch
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    torch.cuda.synchronize()
+    evs[0].record()
+    for i in range(n):
+        step()
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    d = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(n))
+    return {"steps": n, "min_ms": round(d[0], 4), "median_ms": round(d[n // 2], 4), "max_ms": round(d[-1], 4)}
+
+
+def kernel_sum_ms(kern: dict, steps: int) -> float:
+    """The profiled pass's kernel time per step (HIP events around every liblgm_amd launch), for comparison with the
+    timed loop's ms_per_step: the difference is launch gaps, host stalls and non-library work (torch ops)."""
+    return round(sum(ms for _, ms in kern.values()) / max(1, steps), 4)
+
+
 def attention_bench(dev, steps: int = 10):
     """LGM's heaviest MVAttention level (core/unet.py:35-49 at C=512, 32x32, 4 views -> L = 4096 tokens, 16 heads,
     D = 32; 8 objects per GPU as in the 'big' training batch), bf16 fwd+bwd through the HIP kernels, torch SDPA on
@@ -477,6 +499,7 @@ def run(args):
         torch.cuda.synchronize()
     kern = prof.summary()
     prof.close()
+    spread = step_spread(step, args.steps)
 
     # the same steps with bit-reproducible gradients (LGM_RENDER_DETERMINISTIC: int64 fixed-point accumulation,
     # SURVEY §5.2), timed the same way: what making it the default would cost
@@ -527,6 +550,8 @@ def run(args):
                    "scenes_per_gpu": B, "global_batch": POOL_SCENES, "pairs_K_reference_rank0": K,
                    "pairs_binned_rank0": K_binned, "parallelism": f"scene-sharded x{world} (no collective)"},
         "kernels": per_kernel,
+        "step_spread": spread,
+        "profiled_kernel_sum_ms_per_step": kernel_sum_ms(kern, args.steps),
     }
     if det:
         det["slowdown_vs_float_atomics"] = round(det["ms_per_step"] / (1e3 * el / args.steps), 3)
@@ -588,6 +613,7 @@ def run(args):
         torch.cuda.synchronize()
     kern3 = prof3.summary()
     prof3.close()
+    spread3 = step_spread(step3, args.steps)
     if world > 1:  # the all-reduce on its own, same tensor size
         buf = torch.zeros(1, N_GAUSS, 14, device=dev)
         for _ in range(3):
@@ -600,6 +626,7 @@ def run(args):
         "ms_per_step": round(1e3 * el3 / args.steps, 4),
         "Mpixels_per_s": round(VIEWS * P * args.steps / el3 / 1e6, 2),
         "allreduce_ms": round(ar["ms"], 4) if world > 1 else None,
+        "step_spread": spread3, "profiled_kernel_sum_ms_per_step": kernel_sum_ms(kern3, args.steps),
         "kernels": {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in kern3.items()}}
 
     if not args.no_cfg5:  # every rank (its all-reduce is collective)

@@ -104,14 +104,21 @@ int lgm_render_tile_lists(int B, int V, int N, int H, int W, const void *workspa
                           unsigned *ids_out, void *stream);
 int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
                            long long pair_capacity, int *n_contrib_out, float *final_T_out, void *stream);
+/* lgm_render_records: the per-(view, Gaussian) compositing records the binning wrote (upstream's geomBuffer:
+ * means2D, conic_opacity, depths, tile rects), DEVICE, each [B,V,N,...] and each may be NULL:
+ *   P_out [4] = (x, y, A', B'), Q_out [4] = (C', log2 opacity, tau', depth) with the conic pre-scaled as
+ *   A' = -log2(e)/2 A, B' = -log2(e) B, C' = -log2(e)/2 C (tau' likewise; render_common.h rec_p / rec_q);
+ *   rects_out [2] u32 = (x0 | y0 << 16, x1 | y1 << 16 | needle << 31), needle = the record's conic partials are
+ *   accumulated in fp64 (float mode). Invisible records: rects (0, 0). */
+int lgm_render_records(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
+                       long long pair_capacity, float *P_out, float *Q_out, unsigned *rects_out, void *stream);
 
 /* Diagnostics: when diag->render_counters (a DEVICE uint64 buffer, caller-zeroed) is set, that call's render kernels
- * add work counts to it: [0] forward wavefront-entry iterations, [1] accepted (pixel, Gaussian) contributions,
- * [2] backward wavefront-entry iterations, [3] backward (pixel, Gaussian) gradient contributions,
- * [4] dense / [5] sparse wavefront reductions, [6] tile-list entries staged by the forward, [7] max forward
- * iterations of one wavefront; then 8 entries per tile t (B*V*T tiles): s_memrealtime stamps (100 MHz)
- * [8+8t] fwd start, [+1] fwd end, [+2], [+3] unused (the backward keeps per-work-item records), [+4] sort start,
- * [+5] sort end, and [+6] the tile's binned list length; then 8 entries per binning workgroup
+ * record per-workgroup timelines in it: [0..7] section cycles of the LGM_BWD_STAMPS diagnostic build (else unused);
+ * then 8 entries per tile t (B*V*T tiles): s_memrealtime stamps (100 MHz) [8+8t] fwd start, [+1] fwd end,
+ * [+2], [+3] the start / end of preprocess-backward workgroup t (t < its grid), [+4] sort start, [+5] sort end,
+ * [+6] the tile's binned list length, [+7] list entries the forward staged (low 32 bits) and wave 0's
+ * 4-entry steps (high 32 bits); then 8 entries per binning workgroup
  * (room for B*V*ceil(N/512); the binning launch uses its first B*ceil(V/3)*ceil(N/512)): phase stamps [0] start,
  * [1] preprocessed, [2] tile tests done, [3] reserved, [4] end, and [5] its binned pairs; then 4 entries per backward
  * work item: start/end stamps, (entries | chunk << 20 | tile << 40) and one unused -- so the buffer must hold

@@ -117,26 +117,39 @@ def orbit_cameras_batched(elevation, azimuth, radius: float = 1.5, fovy: float =
     elevation and azimuth (degrees; scalars or [V] tensors, broadcast) -> (cam_view [V,4,4], cam_view_proj [V,4,4],
     cam_pos [V,3]) on `device`, in one set of vectorised torch ops instead of V numpy orbit_camera calls, V
     host->device copies and V torch.inverse calls. Same conventions as orbit_camera + cameras_from_c2w (OpenGL
-    look-at, up/forward flipped, cam_view = inverse(c2w)^T, computed in closed form for the rigid pose)."""
-    el = torch.as_tensor(elevation, dtype=torch.float32, device=device)
-    az = torch.as_tensor(azimuth, dtype=torch.float32, device=device)
+    look-at, up/forward flipped, cam_view = inverse(c2w)^T).
+
+    Precision: the pose is formed in float64 and rounded to float32, as orbit_camera does (numpy float64 into a
+    float32 matrix); its inverse is then evaluated in float64 (adjugate of the 3x3 block, exact for the pose as
+    rounded) and rounded once, and likewise cam_view @ proj. So every matrix is the correctly rounded value of the
+    reference recipe's exact result, where torch.inverse / @ in float32 carry a few ulps of their own rounding."""
+    f64 = torch.float64
+    el = torch.as_tensor(elevation, dtype=f64, device=device)
+    az = torch.as_tensor(azimuth, dtype=f64, device=device)
     el, az = torch.broadcast_tensors(el.reshape(-1), az.reshape(-1))
     el, az = torch.deg2rad(el), torch.deg2rad(az)
     campos = torch.stack([radius * torch.cos(el) * torch.sin(az), -radius * torch.sin(el),
                           radius * torch.cos(el) * torch.cos(az)], -1)  # [V, 3], target at the origin
-    up = torch.tensor([0.0, 1.0, 0.0], device=campos.device).expand_as(campos)
+    up = torch.tensor([0.0, 1.0, 0.0], dtype=f64, device=campos.device).expand_as(campos)
     fwd = torch.nn.functional.normalize(campos, dim=-1, eps=1e-20)
     right = torch.nn.functional.normalize(torch.cross(up, fwd, dim=-1), dim=-1, eps=1e-20)
     upv = torch.nn.functional.normalize(torch.cross(fwd, right, dim=-1), dim=-1, eps=1e-20)
-    R = torch.stack([right, -upv, -fwd], -1)  # columns; up and forward flipped (core/provider_lvis.py:205)
+    # the float32 c2w of orbit_camera, up and forward flipped (core/provider_lvis.py:205): exact sign flips
+    R = torch.stack([right, -upv, -fwd], -1).float().double()
+    t = campos.float().double()
+    # inverse of [R t; 0 1] = [R^-1, -R^-1 t]: R^-1 = adj(R) / det(R) in float64
+    c0, c1, c2 = R[:, :, 0], R[:, :, 1], R[:, :, 2]
+    adj_rows = torch.stack([torch.cross(c1, c2, dim=-1), torch.cross(c2, c0, dim=-1), torch.cross(c0, c1, dim=-1)], 1)
+    det = (c0 * adj_rows[:, 0]).sum(-1)
+    Rinv = adj_rows / det[:, None, None]
     V = R.shape[0]
-    w2c = torch.zeros(V, 4, 4, device=campos.device)
-    w2c[:, :3, :3] = R.transpose(1, 2)
-    w2c[:, :3, 3] = -(R.transpose(1, 2) @ campos[:, :, None])[:, :, 0]
+    w2c = torch.zeros(V, 4, 4, dtype=f64, device=campos.device)
+    w2c[:, :3, :3] = Rinv
+    w2c[:, :3, 3] = -(Rinv @ t[:, :, None])[:, :, 0]
     w2c[:, 3, 3] = 1.0
     cam_view = w2c.transpose(1, 2)
-    cam_view_proj = cam_view @ projection_matrix(fovy, znear, zfar).to(campos.device)
-    return cam_view, cam_view_proj, -campos
+    cam_view_proj = cam_view @ projection_matrix(fovy, znear, zfar).to(campos.device, f64)
+    return cam_view.float().contiguous(), cam_view_proj.float().contiguous(), -campos.float()
 
 
 def render_orbit_frames(renderer, gaussians, azimuths, elevation: float = 0.0, radius: float = 1.5,

@@ -442,26 +442,16 @@ __device__ __forceinline__ typename Ty<DT>::V8 tr_frag(const typename Ty<DT>::T 
 // rows of each ds_read_b64_tr_b16 half on disjoint 8-bank ranges: conflict-free. D + 8 (20 / 36 / 68 dwords) was
 // 2-way on both (SQ_LDS_BANK_CONFLICT = half of the forward's LDS cycles, profiles/r02/pmc_attn). Measured
 // (profiles/r02/ab_attn_pad): D = 64 fwd / dQ / dK,dV -5 / -8 / -10 %; D = 32 unchanged.
-#ifndef LGM_ATTN_LDK_PAD
-#define LGM_ATTN_LDK_PAD 16
-#endif
-#ifndef LGM_ATTN_FWD_WPE
-#define LGM_ATTN_FWD_WPE 3
-#endif
-#ifndef LGM_ATTN_BWD_WPE
-#define LGM_ATTN_BWD_WPE 2
-#endif
-#ifndef LGM_ATTN_QS_MIN_GRID
-#define LGM_ATTN_QS_MIN_GRID 512  // two query sub-tiles per wave once the grid has this many workgroups
-#endif
+constexpr int LDK_PAD = 16, FWD_WPE = 3, BWD_WPE = 2;
+constexpr long long QS_MIN_GRID = 512;  // two query sub-tiles per wave once the grid has this many workgroups
 template <int DT, int D, int QS>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LGM_ATTN_FWD_WPE : 1))) void k_attn_fwd2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FWD_WPE : 1))) void k_attn_fwd2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
                                                   const typename Ty<DT>::T *__restrict__ k,
                                                   const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                   typename Ty<DT>::T *__restrict__ o, float *__restrict__ lse) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr int LDK = D + LGM_ATTN_LDK_PAD;          // padded rows (see LGM_ATTN_LDK_PAD)
+    constexpr int LDK = D + LDK_PAD;                   // padded rows (see LDK_PAD)
     constexpr int CH = 64 * D * 2 / 16 / NT;           // 16-B chunks per thread per tile (K or V)
     static_assert(CH >= 1, "tile too small for the loader");
     __shared__ __attribute__((aligned(16))) T Ks[2][64 * LDK];
@@ -634,7 +624,7 @@ struct TileLoader {  // one 64-row tile of up to two [tokens][ld] tensors, CH 16
 
 // dK, dV: grid (ceil(L / (64 KS)), B*H); wavefront w owns keys k0 + 16 s + (lane & 15), s < KS.
 template <int DT, int D, int KS>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LGM_ATTN_BWD_WPE : 1))) void k_attn_dkdv2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BWD_WPE : 1))) void k_attn_dkdv2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
                                                    const typename Ty<DT>::T *__restrict__ k,
                                                    const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                    const typename Ty<DT>::T *__restrict__ dout,
@@ -643,7 +633,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
                                                    typename Ty<DT>::T *__restrict__ dv, long long ldd) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr int LDK = D + LGM_ATTN_LDK_PAD;
+    constexpr int LDK = D + LDK_PAD;
     __shared__ __attribute__((aligned(16))) T Qs[2][64 * LDK];
     __shared__ __attribute__((aligned(16))) T Os[2][64 * LDK];
     __shared__ float sl[2][64], sd[2][64];
@@ -758,7 +748,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
 
 // dQ: grid (ceil(L / (64 QS)), B*H); wavefront w owns query rows q0 + 16 s + (lane & 15), s < QS.
 template <int DT, int D, int QS>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LGM_ATTN_BWD_WPE : 1))) void k_attn_dq2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BWD_WPE : 1))) void k_attn_dq2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
                                                  const typename Ty<DT>::T *__restrict__ k,
                                                  const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                  const typename Ty<DT>::T *__restrict__ dout,
@@ -766,7 +756,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? LG
                                                  typename Ty<DT>::T *__restrict__ dq, long long ldd) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr int LDK = D + LGM_ATTN_LDK_PAD;
+    constexpr int LDK = D + LDK_PAD;
     __shared__ __attribute__((aligned(16))) T Ks[2][64 * LDK];
     __shared__ __attribute__((aligned(16))) T Vs[2][64 * LDK];
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -871,7 +861,7 @@ int fwd_impl(int B, int L, int H, float scale, const void *q, const void *k, con
     if constexpr (DT != LGM_ATTN_F32) {
         // two query sub-tiles per wavefront when the grid stays large enough to fill the chip
         constexpr int QS2 = D <= 64 ? 2 : 1;
-        if (QS2 == 2 && (long long)((L + 127) / 128) * B * H >= LGM_ATTN_QS_MIN_GRID) {
+        if (QS2 == 2 && (long long)((L + 127) / 128) * B * H >= QS_MIN_GRID) {
             dim3 grid((L + 127) / 128, B * H);
             LGM_LAUNCH("k_attn_fwd", st, (k_attn_fwd2<DT, D, QS2><<<grid, NT, 0, st>>>(
                                               L, H, scale, (const T *)q, (const T *)k, (const T *)v, ld, (T *)o, lse)));

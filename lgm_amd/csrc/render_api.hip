@@ -282,6 +282,26 @@ int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *worksp
     return LGM_OK;
 }
 
+int lgm_render_records(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
+                       long long pair_capacity, float *P_out, float *Q_out, unsigned *rects_out, void *stream) {
+    lgm::clear_error();
+    lgm::Layout L;
+    int rc = check_ws(B, V, N, H, W, workspace, workspace_bytes, pair_capacity, L);
+    if (rc) return rc;
+    const size_t BVN = (size_t)B * V * N;
+    const char *ws = (const char *)workspace;
+    hipStream_t st = (hipStream_t)stream;
+    const struct { void *dst; size_t off, bytes; } cp[3] = {
+        {P_out, L.gP, BVN * 16}, {Q_out, L.gQ, BVN * 16}, {rects_out, L.rects, BVN * 8}};
+    for (const auto &c : cp) {
+        if (c.dst && c.bytes && hipMemcpyAsync(c.dst, ws + c.off, c.bytes, hipMemcpyDeviceToDevice, st) != hipSuccess) {
+            lgm::set_error("hipMemcpyAsync failed");
+            return LGM_E_HIP;
+        }
+    }
+    return LGM_OK;
+}
+
 int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
                         const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,

@@ -15,8 +15,6 @@
 //                      composite key (LDS blocks + global merge stages).
 #include "render_common.h"
 
-#include <type_traits>
-
 namespace lgm {
 namespace {
 
@@ -49,22 +47,10 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 // Gaussian found by a head-flag max-scan), so no lane idles behind a large Gaussian; a lane computes its row's exact
 // tile range (BinRec) and records the hits in an LDS hit list with their rank in the tile (returned by the
 // histogram atomic). The emission after the global reservation is a flat loop over that list.
-#ifndef LGM_BIN_THREADS
-#define LGM_BIN_THREADS 512
-#endif
-#ifndef LGM_BIN_PREFETCH
-#define LGM_BIN_PREFETCH 1  // load batch it + 1's Gaussian rows while batch it is preprocessed and tested
-#endif
-#ifndef LGM_BIN_ITERS
-#define LGM_BIN_ITERS 3  // measured: 1 -> 50 us, 2 -> 55, 3 -> 46, 4 -> 58 (cfg3)
-#endif
-#ifndef LGM_BIN_VIEWLOOP
-// 1: a workgroup's BIN_ITERS batches are BIN_ITERS VIEWS of the same BIN_G Gaussians (each Gaussian row loaded once
-// per workgroup instead of once per view: pool 199 -> 193 us, single scene 40.6 -> 38.8 us); 0: BIN_ITERS
-// consecutive Gaussian batches of one view (then the next batch's rows are prefetched, LGM_BIN_PREFETCH)
-#define LGM_BIN_VIEWLOOP 1
-#endif
-constexpr int BIN_THREADS = LGM_BIN_THREADS, BIN_G = BIN_THREADS, BIN_ITERS = LGM_BIN_ITERS;
+// A workgroup's BIN_ITERS batches are BIN_ITERS VIEWS of the same BIN_G Gaussians: each Gaussian row is loaded once
+// per workgroup instead of once per view (pool 199 -> 193 us, single scene 40.6 -> 38.8 us; 1 / 2 / 6 views per
+// workgroup measured slower).
+constexpr int BIN_THREADS = 512, BIN_G = BIN_THREADS, BIN_ITERS = 3;
 constexpr int BIN_HITCAP = BIN_THREADS * 6;  // hit-list capacity (typical: ~4 hits per Gaussian)
 static_assert(BIN_THREADS <= 512, "owner index packs into 9 bits");
 
@@ -95,15 +81,12 @@ __device__ __forceinline__ int wave_incl_max(int v, int /*lane*/) {
     return v;
 }
 
-// k_sort's tile order (LGM_SORT_CENTER): the tiles of a view by distance from the image centre, nearest first.
+// k_sort's tile order: the tiles of a view by distance from the image centre, nearest first.
 // The centre tiles carry the longest lists (the object sits in the middle of the frame), so with the views
 // interleaved (workgroup b sorts rank b / BV of view b % BV) the long sorts start in the first residency round and
 // the short ones fill the second. One binning workgroup writes it at its end: a counting sort of the tiles on their
 // squared centre distance quantised to min(T, BIN_THREADS) buckets, in LDS (hk: >= that + RS-wave sums ints). Ties
 // take atomic slots -- the order only schedules the sorts, every order gives the same result.
-#ifndef LGM_SORT_CENTER
-#define LGM_SORT_CENTER 1
-#endif
 __device__ void center_order(int gx, int T, int *__restrict__ corder, int *hk) {
     const int gy = (T + gx - 1) / gx, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int K = min(T, BIN_THREADS);
@@ -146,13 +129,9 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     __shared__ int s_nhit;
     __shared__ unsigned long long s_tot[2];
     const int T = d.T, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-#if LGM_BIN_VIEWLOOP
     const int vgroups = (d.V + BIN_ITERS - 1) / BIN_ITERS;
     const int b = blockIdx.y / vgroups, vg0 = (blockIdx.y - b * vgroups) * BIN_ITERS;
     int bv = b * d.V + vg0;  // the batch's view (updated per batch; `dest` reads it by reference)
-#else
-    const int bv = blockIdx.y, b = bv / d.V;
-#endif
     const bool lds = T <= LDS_HIST_MAX;
     int *hbase = hist + T, *fill = hist + 2 * T;
     int *cur = tile_count + (size_t)bv * T;
@@ -177,36 +156,22 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         }
     };
     // BIN_ITERS batches per workgroup, one after the other: fewer, longer workgroups (2 per CU: 106 VGPRs at 8 waves
-    // per workgroup) fit the single scene's launch into one round of residency. View loop: the batches are views
-    // of the same Gaussians, whose rows are loaded once; otherwise each batch's rows are loaded during the previous
-    // batch (registers), so only the first batch waits for its loads.
-    float gnext[14];
-    {
-        const int i0 = (LGM_BIN_VIEWLOOP ? blockIdx.x : blockIdx.x * BIN_ITERS) * BIN_G + tid;
-        if (i0 < d.N) load_gaussian(gauss + ((size_t)b * d.N + i0) * 14, gnext);
-    }
+    // per workgroup) fit the single scene's launch into one round of residency. The batches are views of the same
+    // Gaussians, whose rows are loaded once.
+    const int i = blockIdx.x * BIN_G + tid;
+    float g[14];
+    if (i < d.N) load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
     for (int it = 0; it < BIN_ITERS; it++) {
-#if LGM_BIN_VIEWLOOP
     if (vg0 + it >= d.V) break;  // workgroup-uniform (the last view group of a scene may be short)
     bv = b * d.V + vg0 + it;
     cur = tile_count + (size_t)bv * T;
-    const int i = blockIdx.x * BIN_G + tid;
-#else
-    const int i = (blockIdx.x * BIN_ITERS + it) * BIN_G + tid;
-#endif
     if (tid == 0) s_nhit = 0;
     if (lds)
         for (int t = tid; t < T; t += BIN_THREADS) hist[t] = 0;
     // ---- preprocess, one Gaussian per thread
     Geo o;
     bool vis = false;
-    float g[14];
-#pragma unroll
-    for (int q = 0; q < 14; q++) g[q] = gnext[q];
-    if (!LGM_BIN_VIEWLOOP && LGM_BIN_PREFETCH && it + 1 < BIN_ITERS && i + BIN_G < d.N)
-        load_gaussian(gauss + ((size_t)b * d.N + i + BIN_G) * 14, gnext);  // the next batch's row, in flight
     if (i < d.N) {
-        if (!LGM_BIN_VIEWLOOP && !LGM_BIN_PREFETCH && it > 0) load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
         vis = preprocess_one(g, views + 16 * bv, projs + 16 * bv, d, o);
         if (MODE != COUNT) {
             const size_t k = (size_t)bv * d.N + i;
@@ -214,7 +179,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                 const float4 rp = rec_p(o.x, o.y, o.A, o.B), rq = rec_q(o.C, o.opacity, o.tau, o.depth);
                 gP[k] = rp;  // pre-scaled compositing records (render_common.h)
                 gQ[k] = rq;
-                const bool side = ACC_SIDE && !(d.options & LGM_RENDER_DETERMINISTIC) && rec_needle(rp.z, rp.w, rq.x);
+                const bool side = !(d.options & LGM_RENDER_DETERMINISTIC) && rec_needle(rp.z, rp.w, rq.x);
                 rects[k] = make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16),
                                       (unsigned)o.x1 | ((unsigned)o.y1 << 16) | (side ? 0x80000000u : 0u));
                 if (side) {  // the record's fp64 conic accumulators (acc_side_offset)
@@ -223,7 +188,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                 }
                 // the backward's per-view gradient accumulators start at zero (a repeated backward clears them with
                 // LGM_RENDER_BACKWARD_AGAIN); int64 fixed point in deterministic mode
-                if (LGM_ACC_F64 || (d.options & LGM_RENDER_DETERMINISTIC)) {  // 8-B elements (int64 / fp64)
+                if (d.options & LGM_RENDER_DETERMINISTIC) {  // 8-B elements (int64)
                     ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(accum) + k * (NACC_V / 2);
 #pragma unroll
                     for (int q = 0; q < NACC_V / 2; q++) a2[q] = make_ulonglong2(0ull, 0ull);
@@ -240,7 +205,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
             if (radii_out) radii_out[k] = vis ? o.radius : 0;
             if (bv % d.V == 0) {  // the scene's view-independent record (opacity, colour), once per scene
                 const size_t ks = (size_t)d.BV * d.N * NACC_V + ((size_t)b * d.N + i) * NACC_S;
-                if (LGM_ACC_F64 || (d.options & LGM_RENDER_DETERMINISTIC)) {  // 8-B elements (int64 / fp64)
+                if (d.options & LGM_RENDER_DETERMINISTIC) {  // 8-B elements (int64)
                     ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(reinterpret_cast<unsigned long long *>(accum) + ks);
                     a2[0] = make_ulonglong2(0ull, 0ull);
                     a2[1] = make_ulonglong2(0ull, 0ull);
@@ -431,86 +396,24 @@ __global__ __launch_bounds__(1024) void k_scan(const int *__restrict__ count, in
     if (tid == 1023) start[M] = (int)wsum[15];
 }
 
-// LPT order: the (view, tile) work items sorted by decreasing bucket size (counting sort on n / 8). The
-// compositing kernels take their tiles in this order, so the longest lists start first and the short ones fill
-// the gaps (longest-processing-time-first scheduling). One workgroup of NT threads; hist: ORD_BK ints of LDS.
-#ifndef LGM_SORT_LPT
-#define LGM_SORT_LPT 1  // 1: a separate k_order launch before k_sort, whose workgroups then take tiles in LPT order
-#endif
-constexpr int ORD_THREADS = 1024, ORD_BK = 2048;
-template <int NT>
-__device__ __forceinline__ void order_tiles(int M, long long slot_stride, const int *__restrict__ tile_start,
-                                            const int *__restrict__ tile_count, int *__restrict__ order, int *hist,
-                                            int *s_wsum) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int q = tid; q < ORD_BK; q += NT) hist[q] = 0;
-    __syncthreads();
-    auto key = [&](int t) {
-        long long base;
-        int n;
-        tile_range(t, slot_stride, tile_start, tile_count, base, n);
-        return ORD_BK - 1 - min(n >> 3, ORD_BK - 1);  // descending size
-    };
-    for (int t = tid; t < M; t += NT) atomicAdd(&hist[key(t)], 1);
-    __syncthreads();
-    // exclusive scan of ORD_BK counters, ORD_BK / NT per thread
-    constexpr int PER = ORD_BK / NT;
-    int loc[PER], sum = 0;
-#pragma unroll
-    for (int j = 0; j < PER; j++) { loc[j] = hist[tid * PER + j]; sum += loc[j]; }
-    int x = sum;
-#pragma unroll
-    for (int dd = 1; dd < 64; dd <<= 1) {
-        const int y = __shfl_up(x, dd, 64);
-        if (lane >= dd) x += y;
-    }
-    if (lane == 63) s_wsum[w] = x;
-    __syncthreads();
-    int run = x - sum;
-    for (int ww = 0; ww < w; ww++) run += s_wsum[ww];
-#pragma unroll
-    for (int j = 0; j < PER; j++) { hist[tid * PER + j] = run; run += loc[j]; }
-    __syncthreads();
-    for (int t = tid; t < M; t += NT) order[atomicAdd(&hist[key(t)], 1)] = t;
-}
-
-// k_order: the LPT order on its own (only when there is nothing to sort: N == 0; otherwise k_sort's
-// workgroup 0 computes it alongside the tile sorts).
-__global__ __launch_bounds__(ORD_THREADS) void k_order(int M, long long slot_stride, const int *__restrict__ tile_start,
-                                                       const int *__restrict__ tile_count, int *__restrict__ order) {
-    __shared__ int hist[ORD_BK];
-    __shared__ int s_wsum[ORD_THREADS / 64];
-    order_tiles<ORD_THREADS>(M, slot_stride, tile_start, tile_count, order, hist, s_wsum);
-}
-
 // ------------------------------------------------------------------------------------------------------------
 // Per-tile sort: up to RS_CAP entries sorted in LDS (larger buckets take sort_oversized): u32 keys, u16 bucket
 // positions and per-wave 512-bucket counters; 8 rows per lane.
 // RS_CAP is 4032, not 4096: the workgroup's whole LDS (the dynamic image, RS_CAP * 8 + 8 KB on the MSD path, plus
 // ~400 B of static __shared__) must stay <= 40 KB for 4 workgroups per CU (160 KB). At 4096 it was 41,360 B and
 // the kernel ran 3 per CU; lists of 4033..4096 entries now take the (rare) oversized path.
-#ifndef LGM_RS_THREADS
-#define LGM_RS_THREADS 512
-#endif
-#ifndef LGM_RS_CAP
-#define LGM_RS_CAP 4032
-#endif
-constexpr int RS_THREADS = LGM_RS_THREADS, RS_WAVES = RS_THREADS / 64, RS_CAP = LGM_RS_CAP,
+constexpr int RS_THREADS = 512, RS_WAVES = RS_THREADS / 64, RS_CAP = 4032,
               RS_MAXR = (RS_CAP + RS_THREADS - 1) / RS_THREADS;
 constexpr int RS_OBLK = 4096;  // sort_oversized's LDS block (a power of two), u64 keys over the image
 static_assert(RS_CAP <= RS_OBLK && RS_CAP % 64 == 0, "sort image layout");
 constexpr int RS_DBITS = 9, RS_B = 1 << RS_DBITS;  // digit width: a typical 26-bit depth span takes 3 passes
-#ifndef LGM_RS_CNT16
-#define LGM_RS_CNT16 1  // per-wave digit counters as u16 (they never exceed RS_CAP): halves their LDS
-#endif
-typedef std::conditional<LGM_RS_CNT16, unsigned short, int>::type RsCnt;
+typedef unsigned short RsCnt;  // per-wave digit counters as u16 (they never exceed RS_CAP): halves their LDS
 // (the MSD path below takes RS_CAP * 8 + 2048 * 4 bytes of the same block)
 constexpr int RS_LDS_LSD = RS_CAP * 4 + RS_CAP * 2 + RS_WAVES * RS_B * (int)sizeof(RsCnt);
 constexpr int RS_LDS = RS_LDS_LSD > RS_CAP * 8 + 2048 * 4 ? RS_LDS_LSD : RS_CAP * 8 + 2048 * 4;
 static_assert(RS_CAP < 65536, "u16 counters");
 static_assert(RS_LDS >= RS_OBLK * 8, "sort_oversized reuses the image as u64[RS_OBLK]");
-static_assert(RS_CAP > 4032 || RS_LDS + 512 <= 160 * 1024 / 4,  // (larger caps only for A/B timing)
-              "4 sort workgroups per CU (with the static __shared__ words)");
+static_assert(RS_LDS + 512 <= 160 * 1024 / 4, "4 sort workgroups per CU (with the static __shared__ words)");
 static_assert(RS_B % RS_THREADS == 0 || RS_THREADS % RS_B == 0, "bucket scan layout");
 
 __device__ __forceinline__ unsigned long long lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
@@ -683,23 +586,14 @@ __device__ void sort_oversized(unsigned long long *seg, int n, unsigned long lon
 // construction (equal keys share a bucket and are ranked by id), so the result is upstream's order, written as
 // ids straight into the tile's range. Returns false -- nothing written -- when some bucket holds more than
 // MSD_LIMIT entries (clustered depths, e.g. a flat layer facing the camera); the caller then runs the LSD passes.
-// LDS: keys sk [RS_CAP] u32, ids si [RS_CAP] u32, counters hc [MSD_B] u32 (40 KB: 4 workgroups per CU, as the
+// LDS: (key, id) u64 entries [RS_CAP] over the image, counters hc [MSD_B] u32 (40 KB: 4 workgroups per CU, as the
 // 64-VGPR cap allows anyway).
-#ifndef LGM_SORT_MSD
-#define LGM_SORT_MSD 1
-#endif
-#ifndef LGM_SORT_KV
-#define LGM_SORT_KV 1
-#endif
-#ifndef LGM_SORT_LOAD_ALL
-#define LGM_SORT_LOAD_ALL 1
-#endif
 constexpr int MSD_BITS = 11, MSD_B = 1 << MSD_BITS, MSD_LIMIT = 48;
 static_assert(MSD_B % RS_THREADS == 0, "scan layout");
 
 __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const unsigned (&ir)[RS_MAXR], int n,
-                                         int c0, int R, int kbits, unsigned *sk, unsigned *si, unsigned *hc,
-                                         int *s_wsum, int *s_flag, unsigned *__restrict__ ids_out) {
+                                         int c0, int R, int kbits, unsigned *sk, unsigned *hc, int *s_wsum,
+                                         int *s_flag, unsigned *__restrict__ ids_out) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int shift = kbits > MSD_BITS ? kbits - MSD_BITS : 0;
     constexpr int BPT = MSD_B / RS_THREADS;
@@ -732,7 +626,6 @@ __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const un
     }
     __syncthreads();
     // scatter (arbitrary order inside a bucket); afterwards hc[b] is the END of bucket b (= start of b + 1)
-#if LGM_SORT_KV
     // key and id side by side (the sk / si image read as one u64 array): one 8-B LDS write per entry here and one
     // 8-B read per bucket entry in the ranking, on the composite (key << 32 | id) order
     unsigned long long *skv = reinterpret_cast<unsigned long long *>(sk);
@@ -752,29 +645,6 @@ __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const un
         int rank = lo;
         for (int z = lo; z < hi; z++) rank += skv[z] < cq ? 1 : 0;
         ids_out[rank] = (unsigned)cq;
-    }
-    return true;
-#endif
-#pragma unroll
-    for (int r = 0; r < RS_MAXR; r++) {
-        const int e = c0 + r * 64 + lane;
-        if (r < R && e < n) {
-            const unsigned pos = atomicAdd(&hc[kr[r] >> shift], 1u);
-            sk[pos] = kr[r];
-            si[pos] = ir[r];
-        }
-    }
-    __syncthreads();
-    // rank inside the bucket: final position = #(bucket entries before it in (key, id) order) + bucket start
-    for (int q = tid; q < n; q += RS_THREADS) {
-        const unsigned kq = sk[q], iq = si[q], bq = kq >> shift;
-        const int lo = bq ? (int)hc[bq - 1] : 0, hi = (int)hc[bq];
-        int rank = lo;
-        for (int z = lo; z < hi; z++) {
-            const unsigned kz = sk[z];
-            rank += (kz < kq || (kz == kq && si[z] < iq)) ? 1 : 0;
-        }
-        ids_out[rank] = iq;  // the bucket (read only in the load phase, before the barriers above) takes the ids
     }
     return true;
 }
@@ -799,7 +669,6 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     unsigned kr[RS_MAXR], ir[RS_MAXR];
     unsigned short pr[RS_MAXR];
     unsigned lmin = 0xffffffffu, lmax = 0u, vmax = 0u;
-#if LGM_SORT_LOAD_ALL
     // every row's load issued before the first use (clamped index, no per-row branch around the load): with the
     // load inside the per-row branch each row waited for its own round trip (vmcnt(0) per row, R serial trips)
     unsigned long long xv[RS_MAXR];
@@ -808,18 +677,13 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
         const int e = c0 + r * 64 + lane;
         if (r < R) xv[r] = seg[min(e, n - 1)];  // (r < R is workgroup-uniform)
     }
-#endif
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         kr[r] = 0u;
         ir[r] = 0u;
         const int e = c0 + r * 64 + lane;
         if (r < R && e < n) {
-#if LGM_SORT_LOAD_ALL
             const unsigned long long x = xv[r];
-#else
-            const unsigned long long x = seg[e];
-#endif
             kr[r] = (unsigned)(x >> 32);
             ir[r] = (unsigned)x;
             lmin = min(lmin, kr[r]);
@@ -827,24 +691,13 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
             vmax = max(vmax, (unsigned)x);
         }
     }
-#ifdef LGM_TIMING_SORT_NOP  // timing-only diagnostic build: the ids stay unsorted (wrong renders)
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < RS_MAXR; r++) {
-        const int e = c0 + r * 64 + lane;
-        if (r < R && e < n) reinterpret_cast<unsigned *>(seg)[e] = (unsigned)e < n ? (unsigned)seg[0] : 0u;
-    }
-    return;
-#endif
     // the span is reduced through per-wave LDS slots (no initialised LDS atomics, one barrier), and the MSD bucket
     // counters are zeroed under that barrier (none at the start of msd_sort): k_sort 152 -> 150 us on the pool
     if (tid == 0) { s_long = 0; s_flag = 0; }
-#if LGM_SORT_MSD
     {
         unsigned *hc0 = reinterpret_cast<unsigned *>(smem) + 2 * RS_CAP;
         for (int q = tid; q < MSD_B; q += RS_THREADS) hc0[q] = 0u;
     }
-#endif
     __shared__ unsigned s_wmm[3][RS_WAVES];
     lmin = wave_min_u32(lmin);
     lmax = wave_max_u32(lmax);
@@ -872,13 +725,10 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
             }
         }
     };
-#if LGM_SORT_MSD
     // (kr holds key - kmin: the MSD buckets split the tile's span)
-    if (kbits > 0 && msd_sort(kr, ir, n, c0, R, kbits, sk, reinterpret_cast<unsigned *>(smem) + RS_CAP,
-                              reinterpret_cast<unsigned *>(smem) + 2 * RS_CAP, s_wsum, &s_flag,
-                              reinterpret_cast<unsigned *>(seg)))
+    if (kbits > 0 && msd_sort(kr, ir, n, c0, R, kbits, sk, reinterpret_cast<unsigned *>(smem) + 2 * RS_CAP, s_wsum,
+                              &s_flag, reinterpret_cast<unsigned *>(seg)))
         return;
-#endif
     unsigned idr[RS_MAXR];
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) pr[r] = (unsigned short)(c0 + r * 64 + lane);  // bucket positions
@@ -975,26 +825,14 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     }
 }
 
-// k_sort: grid (1 + B*V*T), block RS_THREADS, dynamic LDS RS_LDS bytes. Workgroup 0 computes the LPT order
-// (it reads only the final tile counts, so it runs alongside the sorts and saves a dependent launch); workgroup
-// 1 + t sorts tile t.
-#ifndef LGM_RS_WPE
-#define LGM_RS_WPE 8  // minimum waves per SIMD for k_sort's registers (8: <= 64 VGPRs, 4 WGs per CU with u16 counters; 6: 80)
-#endif
-__global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(LGM_RS_WPE))) void k_sort(int M, long long slot_stride, const int *__restrict__ tile_start,
-                                                     const int *__restrict__ tile_count,
-                                                     unsigned long long *__restrict__ pairs, int *__restrict__ order,
-                                                     unsigned long long *__restrict__ counters, int BV, int T,
-                                                     const int *__restrict__ corder) {
-    if (!LGM_XCD_ORDER && LGM_SORT_LPT == 0 && blockIdx.x == 0) {
-        extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-        static_assert(RS_LDS >= (ORD_BK + RS_WAVES) * 4, "order_tiles reuses the sort image");
-        int *hist = reinterpret_cast<int *>(smem);
-        order_tiles<RS_THREADS>(M, slot_stride, tile_start, tile_count, order, hist, hist + ORD_BK);
-        return;
-    }
-    // LGM_SORT_LPT: k_order ran first and the sorts take their tiles longest first too
-    int tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, M) : LGM_SORT_LPT ? order[blockIdx.x] : (int)blockIdx.x - 1;
+// k_sort: grid (B*V*T), block RS_THREADS, dynamic LDS RS_LDS bytes; workgroup b sorts tile xcd_item(b), or with
+// the centre-first table (center_order) tile corder[b / BV] of view b % BV. 8 waves per SIMD: <= 64 VGPRs, 4
+// workgroups per CU with the u16 counters.
+__global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8))) void k_sort(
+    int M, long long slot_stride, const int *__restrict__ tile_start, const int *__restrict__ tile_count,
+    unsigned long long *__restrict__ pairs, unsigned long long *__restrict__ counters, int BV, int T,
+    const int *__restrict__ corder) {
+    int tile = xcd_item(blockIdx.x, M);
     if (corder) {  // centre-first, views interleaved (center_order)
         const int r = (int)blockIdx.x / BV, v = (int)blockIdx.x - r * BV;
         tile = v * T + corder[r];
@@ -1032,14 +870,10 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     unsigned long long *pairs = (unsigned long long *)(ws + L.pairs), *misc = (unsigned long long *)(ws + L.misc);
     float *accum = (float *)(ws + L.accum);
     const size_t lds = d.T <= LDS_HIST_MAX ? 3 * (size_t)d.T * 4 : 0;
-    // k_sort's centre-first tile table (first T ints of the order buffer, which the XCD order leaves unused; the
-    // binning histogram's 3T ints of LDS hold its counting sort)
-    int *corder = LGM_SORT_CENTER && LGM_XCD_ORDER && lds && d.T >= 8 ? (int *)(ws + L.order) : nullptr;
-#if LGM_BIN_VIEWLOOP
+    // k_sort's centre-first tile table (the first T ints of the order buffer; the binning histogram's 3T ints of LDS
+    // hold its counting sort)
+    int *corder = lds && d.T >= 8 ? (int *)(ws + L.order) : nullptr;
     dim3 grid((d.N + BIN_G - 1) / BIN_G, d.B * ((d.V + BIN_ITERS - 1) / BIN_ITERS));
-#else
-    dim3 grid((d.N + BIN_G * BIN_ITERS - 1) / (BIN_G * BIN_ITERS), d.BV);
-#endif
     if (d.N > 0) {
         if (count_only || !L.slot) {
             LGM_LAUNCH("k_bin_count", st, (k_bin<COUNT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
@@ -1058,22 +892,14 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view,
                            cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum, corder)));
             }
-            if (!LGM_XCD_ORDER && LGM_SORT_LPT) {
-                LGM_LAUNCH("k_order", st, (k_order<<<1, ORD_THREADS, 0, st>>>((int)M, L.slot ? (long long)d.N : -1LL,
-                                                                             tstart, tcount, (int *)(ws + L.order))));
-            }
-            LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M + (!LGM_XCD_ORDER && !LGM_SORT_LPT ? 1 : 0), RS_THREADS, RS_LDS, st>>>(
-                                         (int)M, L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs,
-                                         (int *)(ws + L.order), d.counters, d.BV, d.T, corder)));
+            LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M, RS_THREADS, RS_LDS, st>>>(
+                                         (int)M, L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs, d.counters,
+                                         d.BV, d.T, corder)));
         }
     }
     if (d.N == 0 && !L.slot && hipMemsetAsync(ws + L.tile_start, 0, (M + 1) * 4, st) != hipSuccess) {
         set_error("hipMemsetAsync failed");  // packed mode with no Gaussians: every tile range is empty
         return LGM_E_HIP;
-    }
-    if (!LGM_XCD_ORDER && !count_only && d.N == 0) {  // the compositing kernels index their tiles through it
-        LGM_LAUNCH("k_order", st, (k_order<<<1, ORD_THREADS, 0, st>>>((int)M, L.slot ? (long long)d.N : -1LL,
-                                                                     tstart, tcount, (int *)(ws + L.order))));
     }
     if (stats_out && hipMemcpyAsync(stats_out, ws + L.misc, 16, hipMemcpyDeviceToDevice, st) != hipSuccess) {
         set_error("hipMemcpyAsync failed");

@@ -24,9 +24,9 @@ __host__ __device__ __forceinline__ size_t acc_index(int q, size_t bvN_i, size_t
     return q < 5 ? bvN_i * NACC_V + q : q < 9 ? BVN * NACC_V + bN_i * NACC_S + (q - 5) : bvN_i * NACC_V + 5;
 }
 __host__ __device__ inline size_t acc_elems(size_t B, size_t V, size_t N) { return B * V * N * NACC_V + B * N * NACC_S; }
-// Float mode, LGM_ACC_SIDE: the conic partials (q = 2..4) of NEEDLE records go to fp64 side accumulators, 3 per
-// (view, Gaussian), placed after the fp32 ones (float offset acc_side_offset, 8-B aligned). A needle is a record
-// whose conic condition (A + C)^2 / (AC - B^2) exceeds LGM_ACC_NEEDLE (or is not positive definite), decided on the
+// Float mode: the conic partials (q = 2..4) of NEEDLE records go to fp64 side accumulators, 3 per (view, Gaussian),
+// placed after the fp32 ones (float offset acc_side_offset, 8-B aligned). A needle is a record whose conic
+// condition (A + C)^2 / (AC - B^2) exceeds ACC_NEEDLE (or is not positive definite), decided on the
 // stored record (rec_needle) identically by the binning, the backward's flush and the preprocess backward (via a
 // flag in bit 31 of the record's rect).
 __host__ __device__ inline size_t acc_side_offset(size_t B, size_t V, size_t N) { return (acc_elems(B, V, N) + 1) & ~(size_t)1; }
@@ -34,32 +34,18 @@ constexpr int LDS_HIST_MAX = 8192;                   // tiles per view for the L
 constexpr float LOG2E = 1.4426950408889634f;
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
-// Deterministic mode: every tile owns CK_QUOTA checkpoint slots (its chunk boundaries 1..CK_QUOTA), so how a tile's
-// walk splits into backward work items depends on the tile alone -- not on which tiles won the shared pool's slot
-// counters (a racing split changes the backward's per-chunk partials in their last bits). Boundaries beyond the
-// quota stay inside the previous item. Default 0: one backward item per tile -- in this mode the split costs more
-// than its load balance returns, measured on the pool (profiles/r03/ab_det):
-// deterministic k_render_bwd 1950 / 1306 / 955 / 787 / 685 / 650 us at quota 16 / 8 / 4 / 2 / 1 / 0 (float mode 626).
+// Deterministic mode takes no backward checkpoints: one backward work item per tile, so how a tile's walk splits into
+// work items cannot depend on which tiles won the shared pool's slot counters (a racing split changes the backward's
+// per-chunk partials in their last bits). A per-tile checkpoint quota was measured (profiles/r03/ab_det):
+// deterministic k_render_bwd 1950 / 1306 / 955 / 787 / 685 / 650 us at quota 16 / 8 / 4 / 2 / 1 / 0 (float mode
+// 626) -- in the fixed-point mode the split costs more than its load balance returns.
 // Float mode's gradient accumulators: fp32, and fp64 for the conic partials of needle-like records. A needle's conic
 // partials from different tiles and views largely cancel and the cov2D inverse amplifies what is left (conditions
 // 1e3-2e4), so fp32 atomic sums made its scale / rotation gradients a draw of the atomic order (single runs up to ~3x
 // the fp32 oracle's error vs fp64 at 512^2, profiles/r03/diag_float_spread); fp64 sums of the same fp32 partials are
 // order-independent to ~2^-50 of the partials (the deterministic mode's int64 sums are exact). Measured: all
 // accumulators fp64 +37 us per pool step, the needle side accumulators +24 us (profiles/r03/ab_acc_side).
-#ifndef LGM_ACC_F64
-#define LGM_ACC_F64 0  // every float-mode accumulator fp64
-#endif
-#ifndef LGM_ACC_SIDE
-#define LGM_ACC_SIDE 1  // fp64 side accumulators for the conic partials of needle-like records only
-#endif
-#ifndef LGM_ACC_NEEDLE
-#define LGM_ACC_NEEDLE 300.0f
-#endif
-constexpr bool ACC_SIDE = LGM_ACC_SIDE && !LGM_ACC_F64;
-#ifndef LGM_CK_QUOTA
-#define LGM_CK_QUOTA 0
-#endif
-constexpr int CK_QUOTA = LGM_CK_QUOTA;
+constexpr float ACC_NEEDLE = 300.0f;  // conic condition above which a record's conic partials are summed in fp64
 
 // Workspace layout. Pair storage `pairs` holds one u64 key (depth_bits << 32 | gaussian id) per (Gaussian, tile)
 // pair; after sorting, the tile's u32 ids are written in place at the start of its range.
@@ -70,7 +56,7 @@ struct Layout {
         accum, lossp, lossw, detmax, misc, total;
     long long cap;
     int ck_region;  // backward checkpoint slots per region (8 regions; the forward shards tiles over them)
-    int ck_slots;   // checkpoint slots in all: 8 ck_region, or CK_QUOTA per tile in deterministic mode
+    int ck_slots;   // checkpoint slots in all: 8 ck_region (none in deterministic mode)
     bool slot;
 };
 
@@ -90,9 +76,9 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.tile_count = take(BV * T * 4);
     L.misc = take(64);  // right after tile_count: the binning clears both with one memset (u64 [0..1]: pair
                         // counts of k_bin; u32 [4..11]: the backward-checkpoint region counters; u32 [12]: the
-                        // fused loss reduction's arrival counter)
+                        // fused loss reduction's arrival counter; u32 [13]: deterministic mode's saturated flushes)
     L.tile_start = take((BV * T + 1) * 4);
-    L.order = take(BV * T * 4);
+    L.order = take(T * 4);  // k_sort's centre-first tile table (center_order)
     L.pairs = take((size_t)L.cap * 8);
     L.final_T = take(BV * P * 4);
     L.n_contrib = take(BV * P * 4);
@@ -100,13 +86,12 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.cfin = take(BV * P * 16);  // per-pixel pre-background colour and depth totals (forward -> backward)
     // backward checkpoints (k_render_fwd -> k_render_bwd): 2 per tile on average, 5 planes of 256 floats each
     L.ck_region = (int)((2 * BV * T + 7) / 8);
-    L.ck_slots = det ? (int)(CK_QUOTA * BV * T) : 8 * L.ck_region;
+    L.ck_slots = det ? 0 : 8 * L.ck_region;
     L.ck = take((size_t)L.ck_slots * 5 * TILE_PIX * 4);
     L.cklist = take((size_t)L.ck_slots * 8);
     L.nck = take(BV * T * 4);
     L.cmask = take(BV * P);
-    L.accum = take((det || LGM_ACC_F64) ? acc_elems(B, V, N) * 8
-                                       : acc_side_offset(B, V, N) * 4 + (ACC_SIDE ? BV * N * 3 * 8 : 0));
+    L.accum = take(det ? acc_elems(B, V, N) * 8 : acc_side_offset(B, V, N) * 4 + BV * N * 3 * 8);
     L.lossp = take(BV * T * 2 * 4);  // per-tile sums of squared image / alpha residuals (fused loss)
     L.lossw = take(((BV * T + 2047) / 2048) * 16);  // their per-workgroup double2 partials (k_loss_reduce)
     L.detmax = take(64 * 4);  // deterministic mode: max |dL/dpixel| over the seeds, in 64 atomicMax slots
@@ -260,9 +245,15 @@ __device__ __forceinline__ float4 rec_q(float C, float opacity, float tau, float
 }
 // Needle-like record (see acc_side_offset): on the stored pre-scaled conic A', B', C' (the condition is
 // scale-invariant: (A' + C')^2 / (A'C' - B'^2 / 4) = (A + C)^2 / (AC - B^2)).
+// FP contraction OFF: k_bin evaluates it on the record still in registers (right after the multiplications that
+// form A', B', C'), k_render_bwd on the record loaded back from memory; with contraction a fused multiply-add could
+// round differently in one of them and flip the decision for a record at the threshold. Evaluated as
+// separately rounded IEEE operations it is a pure function of the stored bits in both (tests/test_render_gpu.py
+// test_needle_flag_is_a_function_of_the_stored_record).
 __device__ __forceinline__ bool rec_needle(float Ap, float Bp, float Cp) {
+#pragma clang fp contract(off)
     const float sac = Ap + Cp, dq = Ap * Cp - 0.25f * Bp * Bp;
-    return !(sac * sac <= LGM_ACC_NEEDLE * dq);  // (dq <= 0 or NaN: flagged)
+    return !(sac * sac <= ACC_NEEDLE * dq);  // (dq <= 0 or NaN: flagged)
 }
 __device__ __forceinline__ bool rec_hits_rect(const float4 &p, const float4 &q, float rx0, float rx1, float ry0,
                                               float ry1) {
@@ -402,9 +393,6 @@ __device__ __forceinline__ void tile_range(int tile, long long slot_stride, cons
 // order, and neighbouring tiles -- which gather mostly the same Gaussians -- run on one L2 at about the same time.
 // (The previous LPT order dealt neighbouring tiles to all eight L2s: 5-17 % L2 hit rates in the compositing
 // kernels.) Bijective on [0, M) for any M (group sizes q + 1 for g < r, else q). Speed only, never correctness.
-#ifndef LGM_XCD_ORDER
-#define LGM_XCD_ORDER 1
-#endif
 __host__ __device__ __forceinline__ int xcd_item(int b, int M) {
     const int q = M >> 3, r = M & 7, g = b & 7, i = b >> 3;
     return (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + i;

@@ -12,13 +12,6 @@
 
 #include <type_traits>
 
-#ifndef LGM_LIST_PF
-#define LGM_LIST_PF 1  // per-wave list words read one step ahead (forward)
-#endif
-#ifndef LGM_FWD_FU
-#define LGM_FWD_FU 4  // forward entries evaluated per step: 4 or 8
-#endif
-
 namespace lgm {
 namespace {
 
@@ -84,44 +77,12 @@ struct StageT {                                   // PAD: list padding = entries
     unsigned char mask[ROWS];                 // quadrant mask of the current chunk's entries
     unsigned short list[4][ROWS + PAD];       // per-wave compacted entry indices, padded with the sentinel (ROWS)
 };
-#ifndef LGM_FWD_DB
-#define LGM_FWD_DB 0  // forward staging: 0 synchronous (measured fastest), 1 always prefetching, 2 from the second chunk
-#endif
-using StageFwd = StageT<LGM_FWD_DB ? 2 : 1, LGM_FWD_FU>;
-// the backward sits 3 workgroups per CU only just: its LDS must stay <= 53,744 B (measured: 53,776 B ran at 2)
-#ifndef LGM_BWD_EARLY_STAGE
-#define LGM_BWD_EARLY_STAGE 1  // the first chunk's staging goes out before the per-pixel state loads (bwd 647 -> 644 us)
-#endif
-#ifndef LGM_BWD_PIPE
-#define LGM_BWD_PIPE 1  // software-pipelined moment flush (k_render_bwd): batch k's MFMAs overlap batch k + 1's evaluation
-#endif
-#ifndef LGM_BWD_FLUSH_WAVES
-#define LGM_BWD_FLUSH_WAVES 0  // 1: the gradient atomics on waves 1-3 only, the staging wait on wave 0 only
-                               // (measured slower: 622 -> 694 us on the pool, profiles/r03/ab_bwd_flush)
-#endif
-#ifndef LGM_PREPROC_ACC_EARLY
-#define LGM_PREPROC_ACC_EARLY 1  // preprocess backward: accumulator row loaded beside the rect
-#endif
-#ifndef LGM_BWD_PROLOGUE_FLAT
-#define LGM_BWD_PROLOGUE_FLAT 1  // backward prologue: every per-pixel load issued before the first use
-#endif
-#ifndef LGM_FWD_CK_OPAQUE
-#define LGM_FWD_CK_OPAQUE 1  // forward checkpoint addresses recomputed per chunk (no spilled lane pointer)
-#endif
-#ifndef LGM_BWD_FLUSH_OPAQUE
-#define LGM_BWD_FLUSH_OPAQUE 1  // flush indices recomputed per chunk (no spilled per-lane offsets)
-#endif
-#ifndef LGM_BWD_SPLIT_RN
-#define LGM_BWD_SPLIT_RN 1  // two-term split: round-to-nearest hi (1) or truncated hi (0)
-#endif
-#ifndef LGM_BWD_SPLIT3
-#define LGM_BWD_SPLIT3 0  // moment MFMA operand split: 0 two-term, 1 three-term, 2 three-term in deterministic mode
-#endif
-#ifndef LGM_BWD_CHUNK
-#define LGM_BWD_CHUNK 64  // backward entries per staged chunk (the per-wave moment slots scale with it)
-#endif
-constexpr int BWD_CHUNK = LGM_BWD_CHUNK;
-static_assert(BWD_CHUNK % 64 == 0 && BWD_CHUNK <= TILE_PIX, "chunk rows");
+// Forward: staged synchronously, chunk by chunk (double-buffered staging measured +20 us on the pool: most tiles
+// saturate within a chunk or two, and the prefetch costs LDS and registers); FWD_FU = 4 entries evaluated per step
+// (8 per step spilled). Backward: 64-entry chunks, double-buffered.
+constexpr int FWD_FU = 4;
+using StageFwd = StageT<1, FWD_FU>;
+constexpr int BWD_CHUNK = 64;
 // backward lists are padded to MB with the sentinel: every list position is one MFMA batch column (k_render_bwd)
 using StageBwd = StageT<2, MB, BWD_CHUNK>;
 
@@ -208,7 +169,7 @@ __device__ __forceinline__ int compact_wave(Stage &S, int w, int lane, int jmin 
 }
 
 // U (a multiple of 4) consecutive list entries from kk (a multiple of 4): list_raw reads them (an LDS read that can
-// be issued a step ahead), list_decode makes them wave-uniform (scalar) indices, list_n does both.
+// be issued a step ahead), list_decode makes them wave-uniform (scalar) indices.
 template <int U, class Stage>
 __device__ __forceinline__ void list_raw(const Stage &S, int w, int kk, uint2 (&raw)[U / 4]) {
     static_assert(U % 4 == 0, "list reads are 8-B words");
@@ -226,13 +187,6 @@ __device__ __forceinline__ void list_decode(const uint2 (&raw)[U / 4], int (&jj)
         jj[4 * h + 3] = hi >> 16;
     }
 }
-template <int U, class Stage>
-__device__ __forceinline__ void list_n(const Stage &S, int w, int kk, int (&jj)[U]) {
-    uint2 raw[U / 4];
-    list_raw<U>(S, w, kk, raw);
-    list_decode<U>(raw, jj);
-}
-
 template <class Stage>
 __device__ __forceinline__ void init_sentinel(Stage &S) {
     if (threadIdx.x < sizeof(S.buf) / sizeof(S.buf[0])) {
@@ -243,12 +197,10 @@ __device__ __forceinline__ void init_sentinel(Stage &S) {
     }
 }
 
-// k_render_fwd: grid (B*V*T), block 256.
-#ifndef LGM_FWD_WPE
-#define LGM_FWD_WPE 7  // <= 72 VGPRs (spills outside the compositing loop only): 327 vs 336 us at 6, 411 at 8 (pool)
-#endif
+// k_render_fwd: grid (B*V*T), block 256, tile xcd_item(blockIdx). 7 waves per SIMD: <= 72 VGPRs (spills outside
+// the compositing loop only): 327 vs 336 us at 6, 411 at 8 (pool).
 template <bool LOSS>  // LGM_RENDER_FUSED_LOSS compiled in (its epilogue registers stay out of the plain kernel)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE))) void k_render_fwd(Dims d, long long slot_stride, const int *__restrict__ order,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_render_fwd(Dims d, long long slot_stride,
                                                     const int *__restrict__ tile_start,
                                                     const int *__restrict__ tile_count,
                                                     const unsigned long long *__restrict__ pairs,
@@ -264,7 +216,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
                                                     int ck_region) {
     __shared__ StageFwd S;
     __shared__ int s_ck[2];
-    const int tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, d.BV * d.T) : order[blockIdx.x];
+    const int tile = xcd_item(blockIdx.x, d.BV * d.T);
     const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
     const int tx0 = (t % d.gx) * BX, ty0 = (t / d.gx) * BY;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -283,34 +235,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
     // Tr < 0 marks a saturated pixel (|Tr| its final transmittance): outside pixels start saturated
     float Tr = inside ? 1.0f : -1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     int last = 0;
-    constexpr int FU = LGM_FWD_FU;
-    unsigned c_iter = 0, c_acc = 0, c_list = 0;  // diagnostic work counters (Dims::counters)
-    // Staging: chunk c's entries land by LDS DMA; from chunk PF0 on (a tile that has not saturated after its first
-    // chunk is likely a long one: the critical path of the launch) chunk c+1 streams into the other buffer while c
-    // is composited. Short tiles, most of them, stage synchronously and waste no prefetch. Sorted ids run two
-    // chunks ahead in registers. Each lane tests its own entry as soon as its row has landed, so one barrier
-    // publishes rows and masks together.
-    constexpr int PF0 = LGM_FWD_DB == 1 ? 0 : 1;
+    constexpr int FU = FWD_FU;
+    unsigned c_iter = 0, c_list = 0;  // diagnostic work counters (Dims::counters)
+    // Staging: chunk c's entries land by LDS DMA, synchronously; the sorted ids run two chunks ahead in registers.
+    // Each lane tests its own entry as soon as its row has landed, so one barrier publishes rows and masks together.
     unsigned id_a = tid < n ? ids[tid] : 0u;                        // chunk c
     unsigned id_b = TILE_PIX + tid < n ? ids[TILE_PIX + tid] : 0u;  // chunk c + 1
-    int cur = 0;
-    bool pre = false;  // chunk c was prefetched into S.buf[cur]
     // Backward checkpoints: entering every chunk c >= 1 the per-pixel state (T and the prefix colour / depth sums)
     // goes to a pool slot, reserved one chunk ahead from the region's counter (thread 0), so that k_render_bwd can
     // take the chunk as a work item of its own. The pool is sharded by tile over ckctr's 8 counters; a full region
     // just leaves the rest of the tile to the previous chunk's item.
-    // (XCD order: the region is the tile's block group and its slots are interleaved by region, so the backward's
-    // checkpoint items run on the XCD that composited the tile)
-    const int ck_reg = LGM_XCD_ORDER ? xcd_group(tile, d.BV * d.T) : (tile & 7);
-    const bool det_ck = (d.options & LGM_RENDER_DETERMINISTIC) != 0;  // per-tile checkpoint quota (render_common.h)
+    // (the region is the tile's XCD block group and its slots are interleaved by region, so the backward's
+    // checkpoint items run on the XCD that composited the tile). Deterministic mode takes none (render_common.h).
+    const int ck_reg = xcd_group(tile, d.BV * d.T);
+    const bool det_ck = (d.options & LGM_RENDER_DETERMINISTIC) != 0;
     int ck_slot = -1, ck_written = 0;  // thread 0: slot reserved for the next boundary; checkpoints written
     for (int b0 = 0, c = 0; b0 < n; b0 += TILE_PIX, c++) {
         if (tid == 0) s_ck[c & 1] = ck_slot;  // reserved during chunk c - 1 (its atomic has long returned)
         if (__syncthreads_count(Tr < 0.f) == TILE_PIX) break;  // also: every wave is done with the previous chunk
         c_list += min(TILE_PIX, n - b0);
         const int k = b0 + tid;
-        StageBuf &B = S.buf[cur];
-        if (!pre && k < n) stage_dma(B, w, id_a, gbase, b, d.N, gP, gQ, gauss);
+        StageBuf &B = S.buf[0];
+        if (k < n) stage_dma(B, w, id_a, gbase, b, d.N, gP, gQ, gauss);
         vm_wait_all();
         stage_commit(S, B, tid, k < n, 0u, tx0, ty0, false);
         __syncthreads();
@@ -318,25 +264,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         // chunk's compositing to complete before the next wait
         if (tid == 0) {
             ck_slot = -1;
-            if (b0 + TILE_PIX < n) {
-                if (det_ck) {  // the tile's own quota: boundary c + 1 -> slot tile * CK_QUOTA + c
-                    if (c < CK_QUOTA) ck_slot = tile * CK_QUOTA + c;
-                } else {
-                    const unsigned l = atomicAdd(&ckctr[ck_reg], 1u);
-                    if (l < (unsigned)ck_region)
-                        ck_slot = LGM_XCD_ORDER ? (int)l * 8 + ck_reg : ck_reg * ck_region + (int)l;
-                }
+            if (b0 + TILE_PIX < n && !det_ck) {
+                const unsigned l = atomicAdd(&ckctr[ck_reg], 1u);
+                if (l < (unsigned)ck_region) ck_slot = (int)l * 8 + ck_reg;
             }
         }
         if (c >= 1) {
             const int sl = s_ck[c & 1];  // workgroup-uniform
             if (sl >= 0) {
                 int ctid = tid;
-#if LGM_FWD_CK_OPAQUE
                 // (the lane's checkpoint address recomputed here: hoisted out of the chunk loop, ck + tid was spilled
                 // and its reload's vmcnt(0) waited for the chunk's outstanding loads)
                 asm volatile("" : "+v"(ctid));
-#endif
                 float *cp = ck + (size_t)sl * 5 * TILE_PIX + ctid;
                 cp[0] = fabsf(Tr);
                 cp[TILE_PIX] = C0;
@@ -349,29 +288,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
                 }
             }
         }
-        const bool pf = LGM_FWD_DB != 0 && c >= PF0 && b0 + TILE_PIX < n;  // workgroup-uniform
-        if (pf && k + TILE_PIX < n) stage_dma(S.buf[cur ^ 1], w, id_b, gbase, b, d.N, gP, gQ, gauss);
         id_a = id_b;
         id_b = k + 2 * TILE_PIX < n ? ids[k + 2 * TILE_PIX] : 0u;
-        pre = pf;
-        cur ^= pf ? 1 : 0;
         const int cnt = compact_wave(S, w, lane);
         // FU = 4 entries per step: their alphas are independent of the running transmittance, so they are evaluated
         // together (ILP, branch-free: list padded with the opacity-0 sentinel); only the short T / colour update
         // chain stays serial, in list order, as upstream.
-#if LGM_LIST_PF
         uint2 lraw[FU / 4];  // the next step's list words, read one step ahead (the list is fixed for the chunk)
         list_raw<FU>(S, w, 0, lraw);
-#endif
         for (int kk = 0; kk < cnt; kk += FU) {
             if (__ballot(Tr > 0.f) == 0ull) break;
             c_iter += min(FU, cnt - kk);
             int jj[FU];
-#if LGM_LIST_PF
             list_decode<FU>(lraw, jj);
-#else
-            list_n(S, w, kk, jj);
-#endif
             float al[FU];
             float4 cc[FU], Pv[FU], Qv[FU];
             // all the batch's LDS reads first, then one wait: the scheduler would otherwise interleave them with the
@@ -383,9 +312,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
                 const float4 R = B.R[jj[u]];
                 cc[u] = make_float4(R.x, R.y, R.z, 0.f);
             }
-#if LGM_LIST_PF
             list_raw<FU>(S, w, kk + FU, lraw);  // in bounds: the list rows hold kRows + FU words
-#endif
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < FU; u++) {
@@ -415,17 +342,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
                 Tr = keep ? test_T : -fabsf(Tr);
                 const bool acc = keep && alpha != 0.f;
                 last = acc ? b0 + jj[u] + 1 : last;
-#ifdef LGM_WORK_COUNTERS
-                c_acc += acc ? 1u : 0u;
-#endif
             }
         }
     }
-    if (LGM_FWD_DB != 0 && pre) vm_wait_all();  // no LDS DMA may be in flight when the workgroup retires
     if (tid == 0) {
         if (ck_slot >= 0) cklist[ck_slot] = make_int2(-1, 0);  // reserved for a boundary never reached
-        if (det_ck)  // the rest of the tile's quota: unused
-            for (int j = ck_written; j < CK_QUOTA; j++) cklist[tile * CK_QUOTA + j] = make_int2(-1, 0);
         nck[tile] = ck_written;  // checkpoints c = 1 .. ck_written exist (a prefix: the counters only grow)
     }
     {  // the wave's largest last contributor (outside pixels: 0), for the backward's list bounds
@@ -433,17 +354,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LGM_FWD_WPE
         if (lane == 0) wlast_out[4 * (size_t)tile + w] = wl;
     }
     if (d.counters) {
-        c_acc = (unsigned)__reduce_add_wave(c_acc);
-        if (lane == 0) {
-            atomicAdd(&d.counters[0], (unsigned long long)c_iter);
-            atomicAdd(&d.counters[1], (unsigned long long)c_acc);
-            if (w == 0) atomicAdd(&d.counters[6], (unsigned long long)c_list);
-            atomicMax(&d.counters[7], (unsigned long long)c_iter);
-        }
-        if (tid == 0) {  // per-workgroup timeline (100 MHz s_memrealtime ticks): [8 + 4*tile] start, +1 end
+        // per-workgroup timeline (100 MHz s_memrealtime ticks): [8 + 8 tile] start, +1 end, +7 entries staged (low
+        // 32 bits) and this wave's 4-entry steps (high 32 bits, wave 0). No aggregate atomics on shared words here:
+        // 4 same-address atomics per wave over every tile serialise in L2 and stretched the forward's timeline ~7x.
+        if (tid == 0) {
             d.counters[8 + 8 * (size_t)tile] = t_start;
             d.counters[8 + 8 * (size_t)tile + 1] = __builtin_amdgcn_s_memrealtime();
-            d.counters[8 + 8 * (size_t)tile + 7] = c_list;  // list entries staged (walked) by the forward
+            d.counters[8 + 8 * (size_t)tile + 7] = (unsigned long long)c_list | ((unsigned long long)c_iter << 32);
         }
     }
     float lsq_img = 0.f, lsq_a = 0.f;  // fused loss: this pixel's squared residuals
@@ -595,13 +512,11 @@ __device__ __forceinline__ void pixel_seed(const Dims &d, bool inside, int bv, s
             dp1 = di[P + pid];
             dp2 = di[2 * P + pid];
         }
-#if LGM_BWD_PROLOGUE_FLAT
         unsigned cm = 7u;
         float dd = 0.f, da = 0.f;
         if (d.options & LGM_RENDER_CLAMP_IMAGE) cm = cmask[bv * P + pid];
         if (DEPTH) dd = d_depth[bv * P + pid];
         if (d_alpha) da = d_alpha[bv * P + pid];
-#endif
         if (LOSS) {
             // the MSE seeds (core/models.py:148): dL/dimage += 2 (image - gt) dL/dmse_image / numel, likewise alpha;
             // image recomputed from the forward's totals exactly as the forward formed it
@@ -620,7 +535,6 @@ __device__ __forceinline__ void pixel_seed(const Dims &d, bool inside, int bv, s
             dp2 += s_img * (c2 - (gi[2 * P + pid] * m + bg[2] * (1.f - m)));
             dpa = s_a * ((1 - T_final) - m);
         }
-#if LGM_BWD_PROLOGUE_FLAT
         // (the loads are all issued above, in the blocks that only load: each use waits for the one round trip
         // they share -- with the loads next to their uses, the clamp mask and d_alpha were two serial trips)
         if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // torch clamp gradient: passes where 0 <= x <= 1
@@ -630,16 +544,6 @@ __device__ __forceinline__ void pixel_seed(const Dims &d, bool inside, int bv, s
         }
         if (DEPTH) dpd = dd;
         dpa += da;
-#else
-        if (d.options & LGM_RENDER_CLAMP_IMAGE) {  // torch clamp gradient: passes where 0 <= x <= 1
-            const unsigned m = cmask[bv * P + pid];
-            dp0 = (m & 1u) ? dp0 : 0.f;
-            dp1 = (m & 2u) ? dp1 : 0.f;
-            dp2 = (m & 4u) ? dp2 : 0.f;
-        }
-        if (DEPTH) dpd = d_depth[bv * P + pid];
-        if (d_alpha) dpa += d_alpha[bv * P + pid];
-#endif
     }
     o.dp0 = dp0; o.dp1 = dp1; o.dp2 = dp2; o.dpd = dpd; o.dpa = dpa;
     o.cf = cf;
@@ -751,13 +655,11 @@ __global__ __launch_bounds__(256) void k_det_seed_max(Dims d, const float *__res
 // (columns 0..MB-1) and u (columns MB..) to a per-wave LDS image and sums them with v_mfma_f32_16x16x32_bf16 (the
 // geometric features are exact in bf16; w, u and dL/dC as hi + lo bf16 pairs, ~2^-16 relative per product). Moments are combined over the tile's four waves in LDS, turned into gradient partials per
 // entry and flushed once per (chunk, entry) to the per-view accumulators.
-#ifndef LGM_BWD_WPE
-#define LGM_BWD_WPE 4  // minimum waves per SIMD the register allocation must allow (4: <= 128 VGPRs; the 64-entry
-                       // chunks' LDS admits 4 workgroups per CU)
-#endif
+// Occupancy: at least 4 waves per SIMD for the register allocation (<= 128 VGPRs; the 64-entry chunks' LDS admits 4
+// workgroups per CU); 2 for the depth-gradient instantiation, which LGM never runs.
 template <bool DEPTH, bool LOSS, bool DET>  // DET: LGM_RENDER_DETERMINISTIC (int64 fixed-point flush)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 : LGM_BWD_WPE))) void k_render_bwd(
-    Dims d, long long slot_stride, const int *__restrict__ order, const int *__restrict__ tile_start,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 : 4))) void k_render_bwd(
+    Dims d, long long slot_stride, const int *__restrict__ tile_start,
     const int *__restrict__ tile_count, const unsigned long long *__restrict__ pairs, const float4 *__restrict__ gP,
     const float4 *__restrict__ gQ, const float *__restrict__ gauss, const float *__restrict__ bg,
     const float *__restrict__ final_T, const int *__restrict__ n_contrib, const int *__restrict__ wlast_fwd,
@@ -765,7 +667,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const int *__restrict__ nck,
     const unsigned *__restrict__ ckctr, int ck_region, const float *__restrict__ d_img,
     const float *__restrict__ d_depth, const float *__restrict__ d_alpha, const unsigned char *__restrict__ cmask,
-    float *__restrict__ accum, const unsigned *__restrict__ det_max, long long item_stamps) {
+    float *__restrict__ accum, const unsigned *__restrict__ det_max, unsigned *__restrict__ det_sat,
+    long long item_stamps) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
     constexpr int CH = BWD_CHUNK, LS = CH + 1;  // entries per staged chunk; padded LDS row stride
     __shared__ StageBwd S;
@@ -778,21 +681,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     constexpr int NC = DEPTH ? 4 : 3, NROW = 6 + 2 * NC;
     __shared__ __attribute__((aligned(16))) float sAccW[4][LS * (NROW + 1)];
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
-    __shared__ int s_ndl;  // the chunk holds a needle-like record (ACC_SIDE)
+    __shared__ int s_ndl;  // the chunk holds a needle-like record (its conic partials go to the fp64 side block)
 
     // ---- work item: (tile, chunk c, checkpoint slot)
-    const int M = d.BV * d.T, Mp = LGM_XCD_ORDER ? round8(M) : M;  // head items, then the checkpoint items
+    const int M = d.BV * d.T, Mp = round8(M);  // head items, then the checkpoint items (none in deterministic mode)
     int tile, c = 0, slot = -1;
     if ((int)blockIdx.x < M) {
-        tile = LGM_XCD_ORDER ? xcd_item(blockIdx.x, M) : order[blockIdx.x];
+        tile = xcd_item(blockIdx.x, M);
     } else {
         if ((int)blockIdx.x < Mp) return;  // padding: the checkpoint items start at a multiple of 8
         slot = (int)blockIdx.x - Mp;
-        if (!DET) {  // (deterministic mode: every slot is written, used or not)
-            const int region = LGM_XCD_ORDER ? (slot & 7) : slot / ck_region;
-            const int l = LGM_XCD_ORDER ? (slot >> 3) : slot - region * ck_region;
-            if (l >= (int)ckctr[region]) return;  // an unused slot (workgroup-uniform)
-        }
+        if ((int)(slot >> 3) >= (int)ckctr[slot & 7]) return;  // an unused slot of region slot & 7 (workgroup-uniform)
         const int2 e = cklist[slot];
         if (e.x < 0) return;  // reserved, never written
         tile = e.x;
@@ -810,7 +709,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     int n;
     tile_range(tile, slot_stride, tile_start, tile_count, base, n);
     const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base);
-#if LGM_BWD_EARLY_STAGE
     // the first chunk's ids and LDS DMA go out before the per-pixel state loads (bounded by the list length n, a
     // superset of [s0, s1): rows past s1 are staged but never listed or flushed), so their two dependent memory
     // round trips overlap the pixel loads instead of following them
@@ -819,12 +717,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     unsigned id_cur = stager && s0e + tid < n ? ids[s0e + tid] : 0u;
     if (stager && s0e + tid < n) stage_dma(S.buf[0], w, id_cur, (size_t)bv * d.N, b, d.N, gP, gQ, gauss);
     unsigned id_next = stager && s0e + BWD_CHUNK + tid < n ? ids[s0e + BWD_CHUNK + tid] : 0u;
-#endif
     const size_t P = (size_t)d.H * d.W;
     const size_t pid = inside ? (size_t)d.W * py + px : 0;
     const float T_final = inside ? final_T[bv * P + pid] : 0.f;
     const int last = inside ? n_contrib[bv * P + pid] : 0;
-#if LGM_BWD_PROLOGUE_FLAT
     // the checkpoint's loads go out before the seeds' (one shared round trip instead of a third serial one)
     float ckT = 1.0f, ck1 = 0.f, ck2 = 0.f, ck3 = 0.f, ck4 = 0.f;
     if (slot >= 0) {
@@ -835,27 +731,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         ck3 = cp[3 * TILE_PIX + tid];
         if (DEPTH) ck4 = cp[4 * TILE_PIX + tid];
     }
-#endif
     PixelSeed sd;
     pixel_seed<DEPTH, LOSS>(d, inside, bv, P, pid, T_final, bg, cfin, d_img, d_depth, d_alpha, cmask, sd);
     const float dp0 = sd.dp0, dp1 = sd.dp1, dp2 = sd.dp2, dpd = sd.dpd, dpa = sd.dpa;
     const float4 cf = sd.cf;
     // per-pixel state entering the chunk: the forward's checkpoint (or the list head)
     float Tr = 1.0f, Dup = 0.f;
-#if LGM_BWD_PROLOGUE_FLAT
     if (slot >= 0) {
         Tr = ckT;
         Dup = fmaf(ck1, dp0, fmaf(ck2, dp1, ck3 * dp2));
         if (DEPTH) Dup = fmaf(ck4, dpd, Dup);
     }
-#else
-    if (slot >= 0) {
-        const float *cp = ck + (size_t)slot * 5 * TILE_PIX;
-        Tr = cp[tid];
-        Dup = fmaf(cp[TILE_PIX + tid], dp0, fmaf(cp[2 * TILE_PIX + tid], dp1, cp[3 * TILE_PIX + tid] * dp2));
-        if (DEPTH) Dup = fmaf(cp[4 * TILE_PIX + tid], dpd, Dup);
-    }
-#endif
     init_sentinel(S);  // (published by the first barrier of the chunk loop)
     // the forward's per-wave maxima of the last contributors: positions >= wlast touch no pixel of this wave, and
     // entries behind every pixel's last contributor are never visited
@@ -863,21 +749,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const int wlast = w == 0 ? wl4.x : w == 1 ? wl4.y : w == 2 ? wl4.z : wl4.w;
     const int nlist = min(n, max(max(wl4.x, wl4.y), max(wl4.z, wl4.w)));
     const int s0 = c * TILE_PIX;
-#if LGM_BWD_EARLY_STAGE
-    if (s0 >= nlist) {  // workgroup-uniform
+    if (s0 >= nlist) {  // workgroup-uniform (the early DMA must land before the workgroup retires)
         vm_wait_all();
         return;
     }
-#else
-    if (s0 >= nlist) return;  // workgroup-uniform
-#endif
     const int s1 = (c + 1 <= nck[tile]) ? min(nlist, s0 + TILE_PIX) : nlist;
-#if LGM_BWD_EARLY_STAGE
-    if (s0 >= s1) {  // (nothing to do; the early DMA must land before the workgroup retires)
+    if (s0 >= s1) {  // (nothing to do; likewise)
         vm_wait_all();
         return;
     }
-#endif
     const unsigned long long t_item = d.counters ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #ifdef LGM_BWD_STAMPS  // section cycles of this wave (diagnostic build; counters [2..6], scripts/diag_bwd_stamps.py)
     unsigned long long sec[5] = {0, 0, 0, 0, 0};
@@ -943,11 +823,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // Moment precision. On needle-like footprints (conic condition > ~1e3) the cov2D inverse amplifies any rounding
     // of the conic gradients into their scale / rotation gradients. A two-term split with a TRUNCATED hi part biases
     // every product's rounding one way (~2^-16, coherent over a tile's pixels): at 512^2 it left mean / scale / rot
-    // at ~2x the fp32 oracle's own error vs fp64. Round-to-nearest hi (LGM_BWD_SPLIT_RN, same instruction count:
-    // <= 2^-17 per product, unbiased) and the exact three-term split (+2 MFMAs and +40 VALU per 8-entry batch,
-    // k_render_bwd +7 % on the pool) both put them at 0.5-0.8x the oracle's (profiles/r03/diag_float_spread), so
-    // the two-term round-to-nearest split is the default in both modes.
-    constexpr bool SPLIT3 = LGM_BWD_SPLIT3 == 1 || (LGM_BWD_SPLIT3 == 2 && DET);
+    // at ~2x the fp32 oracle's own error vs fp64. A round-to-nearest hi part (same instruction count: <= 2^-17 per
+    // product, unbiased) and an exact three-term split (+2 MFMAs and +40 VALU per 8-entry batch, k_render_bwd +7 %
+    // on the pool) both put them at 0.5-0.8x the oracle's (profiles/r03/diag_float_spread), so the two-term
+    // round-to-nearest split is used in both modes.
     // B operand of the current batch: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t)
     auto read_batch = [&](float (&xs)[2][8]) {
 #pragma unroll
@@ -961,36 +840,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // split hi + lo, the moment MFMAs, and the lane's (at most 4) live results into this wave's slots
     auto mfma_batch = [&](const float (&xs)[2][8], int col) {
         f32x4 a2[2];
-        if (SPLIT3) {
 #pragma unroll
         for (int t2 = 0; t2 < 2; t2++) {
-            // hi = the top 16 bits, mid = the top 16 bits of the (exact) remainder, lo = what is left (<= 8
-            // significant bits: exact in bf16): hi + mid + lo = x, so the geometric moments (A exact in bf16) are
-            // fp32 accumulations of exact products
-            bf16x8 bh, bm, bl;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const unsigned ub = __builtin_bit_cast(unsigned, xs[t2][j]);
-                bh[j] = __builtin_bit_cast(__bf16, (unsigned short)(ub >> 16));
-                const float r1 = xs[t2][j] - __builtin_bit_cast(float, ub & 0xffff0000u);
-                const unsigned ur = __builtin_bit_cast(unsigned, r1);
-                bm[j] = __builtin_bit_cast(__bf16, (unsigned short)(ur >> 16));
-                bl[j] = (__bf16)(r1 - __builtin_bit_cast(float, ur & 0xffff0000u));
-            }
-            f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
-            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);
-            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bm, cacc, 0, 0, 0);
-            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, cacc, 0, 0, 0);
-            a2[t2] = cacc;
-        }
-        } else {
-#pragma unroll
-        for (int t2 = 0; t2 < 2; t2++) {
-            bf16x8 bh, bl;
-#if LGM_BWD_SPLIT_RN
             // hi = x rounded to bf16 (|x - hi| <= 2^-9 |x|), lo = the exact remainder rounded: <= 2^-17 |x| per
-            // product, half the truncated split's bound at the same instruction count (per pair: two packed
-            // conversions, the two hi halves back to fp32 by a shift and a mask, two subtractions)
+            // product (per pair: two packed conversions, the two hi halves back to fp32 by a shift and a mask, two
+            // subtractions)
+            bf16x8 bh, bl;
 #pragma unroll
             for (int j = 0; j < 8; j += 2) {
                 const bf16x2v hp = __builtin_convertvector((f32x2v){xs[t2][j], xs[t2][j + 1]}, bf16x2v);
@@ -1002,20 +857,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 bl[j] = lp[0];
                 bl[j + 1] = lp[1];
             }
-#else
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                // hi = the top 16 bits (exact truncation), lo = the rest rounded: <= 2^-16 |x| per product
-                const unsigned ub = __builtin_bit_cast(unsigned, xs[t2][j]);
-                bh[j] = __builtin_bit_cast(__bf16, (unsigned short)(ub >> 16));
-                bl[j] = (__bf16)(xs[t2][j] - __builtin_bit_cast(float, ub & 0xffff0000u));
-            }
-#endif
             f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);
             cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, cacc, 0, 0, 0);
             a2[t2] = cacc;
-        }
         }
         const f32x4 acc = a2[0] + a2[1];
         // D[row = 4 qk + r][col = ql]: moments 0..5 in the w columns, rows 6..9 in the u columns; each lane stores its
@@ -1023,25 +868,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #pragma unroll
         for (int rr = 0; rr < 4; rr++) myAcc[mrow[rr] + col] = acc[rr];  // (sentinel columns: row CH, all zero)
     };
-#if !LGM_BWD_PIPE
-    auto flush_batch = [&]() {
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        float xs[2][8];
-        read_batch(xs);
-        mfma_batch(xs, myj);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    };
-#endif
 
     // Staging pipeline (front to back over [s0, s1)): chunk b0 + CH streams into the other buffer by LDS DMA
     // during chunk b0's compositing and is complete (vm_wait_all) before chunk b0's gradient atomics are issued,
     // so no staging load queues behind them; the sorted ids run one chunk further ahead in a register.
-#if !LGM_BWD_EARLY_STAGE
-    const bool stager = tid < CH;  // the threads that stage (and test) one chunk row each
-    unsigned id_cur = stager && s0 + tid < s1 ? ids[s0 + tid] : 0u;
-    if (stager && s0 + tid < s1) stage_dma(S.buf[0], w, id_cur, gbase, b, d.N, gP, gQ, gauss);
-    unsigned id_next = stager && s0 + CH + tid < s1 ? ids[s0 + CH + tid] : 0u;
-#endif
     vm_wait_all();
     int cur = 0;
 #ifdef LGM_BWD_STAMPS
@@ -1055,11 +885,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         __syncthreads();
         const int k = b0 + tid;
         auto &B = S.buf[cur];
-#if LGM_BWD_CHUNK == 64
         // one row per lane: every wave tests all CH entries against its OWN quadrant (one ellipse test per lane
         // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
         if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
-        if (ACC_SIDE && !DET && tid == 0) s_ndl = 0;  // (published by the barrier after the quadrant tests)
+        if (!DET && tid == 0) s_ndl = 0;  // (published by the barrier after the quadrant tests)
         {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
             static_assert((4 * LS * (NROW + 1)) % 4 == 0, "slot zeroing by float4");
             float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
@@ -1083,19 +912,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
         id_cur = id_next;
         id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
-#else
-        if (stager) stage_commit(S, B, tid, k < s1, id_cur, tx0, ty0, true);
-        {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
-            static_assert((4 * LS * (NROW + 1)) % 4 == 0, "slot zeroing by float4");
-            float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
-            for (int q = tid; q < 4 * LS * (NROW + 1) / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        __syncthreads();
-        if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
-        id_cur = id_next;
-        id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
-        const int cnt = compact_wave(S, w, lane, 0, wlast - b0);  // positions < wlast only
-#endif
         static_assert(MB == 8, "one batch = two 4-entry list words");
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c1);
@@ -1151,7 +967,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 }
             }
         };
-#if LGM_BWD_PIPE
         // software-pipelined: batch k's B operand is read from the WU image BEFORE batch k + 1 overwrites it (a
         // wave's LDS operations complete in issue order), so batch k's LDS round trip and moment MFMAs overlap batch
         // k + 1's evaluations instead of stalling the wave between batches
@@ -1168,12 +983,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         }
-#else
-        for (int kk = 0; kk < cnt; kk += MB) {
-            eval_batch(kk);
-            flush_batch();
-        }
-#endif
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c2);
         SEC_ADD(sec[2], ts_c1, ts_c2);  // the entries loop (evaluation, moments)
@@ -1216,7 +1025,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #pragma unroll
                 for (int qq = 0; qq < NV; qq++) part[qq] = ldexpf(part[qq], det_s + (qq < 5 ? nm.k[qq] : 0));
             }
-            if (ACC_SIDE && !DET) {  // a needle's conic partials move to the (dead) lo rows NV.. for the fp64 flush
+            if (!DET) {  // a needle's conic partials move to the (dead) lo rows NV.. for the fp64 flush
                 const bool ndl = rec_needle(Pj.z, Pj.w, Qj.x);
 #pragma unroll
                 for (int qq = 2; qq <= 4; qq++) {
@@ -1232,52 +1041,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         SEC_T(ts_c3);
         SEC_ADD(sec[3], ts_c2, ts_c3);  // barrier + moments -> partials
 #endif
-        // the next chunk's DMA and ids have landed before the atomics below go out (they cannot delay it).
-        // LGM_BWD_FLUSH_WAVES: only wave 0 -- the stager -- waits, and only waves 1-3 issue the atomics: vmcnt is
-        // per wave and in order, so a wave that issued atomics would wait for them too at the next DMA wait
-        if (!LGM_BWD_FLUSH_WAVES || w == 0) vm_wait_all();
+        // the next chunk's DMA and ids have landed before the atomics below go out (they cannot delay it)
+        vm_wait_all();
         __syncthreads();
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
-        constexpr int FT = LGM_BWD_FLUSH_WAVES ? 192 : 256;  // flushing threads
-        int ftid = tid;
-#if LGM_BWD_FLUSH_OPAQUE
+        constexpr int FT = 256;  // flushing threads
+        int ft = tid;
         // the lane's (entry, partial) indices recomputed per chunk: hoisted out of the chunk loop, their 64-bit
         // per-scene accumulator offsets were spilled, and each reload's vmcnt(0) waited for this flush's earlier atomics
-        asm volatile("" : "+v"(ftid));
-#endif
-        const int ft = LGM_BWD_FLUSH_WAVES ? ftid - 64 : ftid;
+        asm volatile("" : "+v"(ft));
 #pragma unroll
         for (int it = 0; it < (CH * NACC + FT - 1) / FT; it++) {
             const int f = it * FT + ft;
             const int j = f / NACC, q = f - j * NACC;
-            if (ft >= 0 && q < NV && j < CH && b0 + j < s1) {
+            if (q < NV && j < CH && b0 + j < s1) {
                 const float a = sAccW[0][q * LS + j];
                 const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
                 const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
-#ifdef LGM_TIMING_NO_ATOMICS  // timing-only build: the flush's atomics become plain stores of the same shape
                 if (a != 0.f) {
-                    if (LGM_ACC_F64) reinterpret_cast<double *>(accum)[ai] = a;
-                    else accum[ai] = a;
-                }
-                if (false) {
-#else
-                if (a != 0.f) {
-#endif
-                    if (DET)  // integer adds commute: order-independent sums (a is already in fixed-point units)
+                    if (DET) {  // integer adds commute: order-independent sums (a is already in fixed-point units)
+                        // (the design bound is |a| <= ~2^51 per flush, so sums of 2^11 flushes stay below 2^63; a
+                        // flush beyond 2^62 breaks it -- counted, and k_preproc_bwd then poisons the call's
+                        // gradients with NaN instead of returning silently wrapped sums)
+                        if (!(fabsf(a) <= 0x1p62f)) atomicAdd(det_sat, 1u);
                         atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
                                   (unsigned long long)__float2ll_rn(fminf(fmaxf(a, -9.0e18f), 9.0e18f)));
-                    else if (LGM_ACC_F64)  // (global_atomic_add_f64)
-                        atomicAdd(reinterpret_cast<double *>(accum) + ai, (double)a);
-                    else
+                    } else {
                         atomicAdd(accum + ai, a);
+                    }
                 }
             }
         }
-        if (ACC_SIDE && !DET && s_ndl) {  // (workgroup-uniform) the chunk's needle conic partials, fp64
+        if (!DET && s_ndl) {  // (workgroup-uniform) the chunk's needle conic partials, fp64
             int tt = tid;
             asm volatile("" : "+v"(tt));  // (recomputed here: lane indices hoisted out of the chunk loop spilled)
-            if (tt < 3 * CH) {
+            for (; tt < 3 * CH; tt += 256) {  // (one pass at CH <= 85)
                 const int j = tt % CH, c3 = tt / CH;
                 const float a = sAccW[0][(NV + c3) * LS + j];
                 if (a != 0.f && b0 + j < s1) {
@@ -1310,10 +1109,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 // The preprocess backward's recomputation of the forward's projection (make_proj / cov2d / the homogeneous
 // divide): FP contraction on and 1-ulp v_rcp_f32 reciprocals. The forward keeps the oracle's bit-exact operation
 // order because its integer outputs (radii, tile rects, sort keys) depend on it; here the values only feed
-// gradients, and each IEEE division is ~10 VALU of a single thread's serial view chain.
-#ifndef LGM_PREPROC_FAST
-#define LGM_PREPROC_FAST 1
-#endif
+// gradients, and each IEEE division is ~10 VALU of a single thread's serial view chain (k_preproc_bwd 61.1 -> 55.5 us
+// on the pool, gradients as accurate or more: profiles/r03/ab_preproc_fast).
 __device__ __forceinline__ ProjCtx make_proj_bwd(const float *Vw, float mx, float my, float mz, float fx, float fy,
                                                  float tanx, float tany) {
     ProjCtx P;
@@ -1356,9 +1153,11 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
                                                      float *__restrict__ accum, float *__restrict__ d_gauss,
                                                      float *__restrict__ d_means2D, const float4 *__restrict__ gP,
                                                      const float4 *__restrict__ gQ,
-                                                     const unsigned *__restrict__ det_max) {
+                                                     const unsigned *__restrict__ det_max,
+                                                     const unsigned *__restrict__ det_sat) {
     const bool det = (d.options & LGM_RENDER_DETERMINISTIC) != 0;
     const int det_s = det ? det_seed_shift(det_max) : 0;
+    const bool det_bad = det && *det_sat != 0u;  // a fixed-point flush overflowed (k_render_bwd): poison the call
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
     // diagnostics: workgroup g's start / end in slots [2], [3] of per-tile record g (unused by the other kernels)
@@ -1381,16 +1180,14 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         const int bv = b * d.V + v;
         const size_t k = (size_t)bv * d.N + i;
         const uint2 r = rects[k];
-#if LGM_PREPROC_ACC_EARLY
         // float mode: the accumulator row is loaded beside the rect, not after it (one memory round trip per view
         // instead of two; an invisible view's row is uninitialised workspace, loaded and dropped)
         float2 acc_e[NACC_V / 2];
-        if (!det && !LGM_ACC_F64) {
+        if (!det) {
             const float2 *acc2 = reinterpret_cast<const float2 *>(accum + k * NACC_V);
 #pragma unroll
             for (int q = 0; q < NACC_V / 2; q++) acc_e[q] = acc2[q];
         }
-#endif
         const bool vis = (r.x & 0xffff) != (r.y & 0xffff);
         if (!vis) {
             if (d_means2D) { d_means2D[2 * k] = 0.f; d_means2D[2 * k + 1] = 0.f; }
@@ -1407,29 +1204,14 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
                 acc[2 * q] = (float)ldexp((double)a.x, -(det_s + nm.k[2 * q]));
                 acc[2 * q + 1] = (float)ldexp((double)a.y, -(det_s + nm.k[2 * q + 1]));
             }
-        } else if (LGM_ACC_F64) {
-            const double2 *acc2 = reinterpret_cast<const double2 *>(accum) + k * (NACC_V / 2);
+        } else {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
 #pragma unroll
-            for (int q = 0; q < NACC_V / 2; q++) {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
-                const double2 a = acc2[q];
-                acc[2 * q] = (float)a.x;
-                acc[2 * q + 1] = (float)a.y;
-            }
-        } else {
-            const float2 *acc2 = reinterpret_cast<const float2 *>(accum + k * NACC_V);
-#pragma unroll
-            for (int q = 0; q < NACC_V / 2; q++) {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
-#if LGM_PREPROC_ACC_EARLY
-                const float2 a = acc_e[q];
-                (void)acc2;
-#else
-                const float2 a = acc2[q];
-#endif
-                acc[2 * q] = a.x;
-                acc[2 * q + 1] = a.y;
+            for (int q = 0; q < NACC_V / 2; q++) {
+                acc[2 * q] = acc_e[q].x;
+                acc[2 * q + 1] = acc_e[q].y;
             }
         }
-        if (ACC_SIDE && !det && (r.y >> 31)) {  // a needle: its conic partials were summed in fp64
+        if (!det && (r.y >> 31)) {  // a needle: its conic partials were summed in fp64
             const double *sd = reinterpret_cast<const double *>(accum + acc_side_offset(d.B, d.V, d.N)) + k * 3;
             acc[2] = (float)sd[0];
             acc[3] = (float)sd[1];
@@ -1442,19 +1224,11 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         const float *Vw = views + 16 * bv;
         const float *Pm = projs + 16 * bv;
         // ---- cov2D backward
-#if LGM_PREPROC_FAST
         const ProjCtx Pc = make_proj_bwd(Vw, g[0], g[1], g[2], fx, fy, d.tanx, d.tany);
         float a, bb, c;
         cov2d_bwd(Pc, c3, a, bb, c);
         const float denom = a * c - bb * bb;
         const float denom2inv = __builtin_amdgcn_rcpf((denom * denom) + 0.0000001f);
-#else
-        const ProjCtx Pc = make_proj(Vw, g[0], g[1], g[2], fx, fy, d.tanx, d.tany);
-        float a, bb, c;
-        cov2d(Pc, c3, a, bb, c);
-        const float denom = a * c - bb * bb;
-        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-#endif
         float dL_da = 0, dL_db = 0, dL_dc = 0;
         if (denom2inv != 0) {
             dL_da = denom2inv * (-c * c * dcx + 2 * bb * c * dcy + (denom - a * c) * dcz);
@@ -1480,7 +1254,7 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         const float dJ02 = Vw[2] * dT0[0] + Vw[6] * dT0[1] + Vw[10] * dT0[2];
         const float dJ11 = Vw[1] * dT1[0] + Vw[5] * dT1[1] + Vw[9] * dT1[2];
         const float dJ12 = Vw[2] * dT1[0] + Vw[6] * dT1[1] + Vw[10] * dT1[2];
-        const float tz = LGM_PREPROC_FAST ? __builtin_amdgcn_rcpf(Pc.t[2]) : 1.f / Pc.t[2], tz2 = tz * tz, tz3 = tz2 * tz;
+        const float tz = __builtin_amdgcn_rcpf(Pc.t[2]), tz2 = tz * tz, tz3 = tz2 * tz;
         const float dtx = Pc.xmul * -fx * tz2 * dJ02;
         const float dty = Pc.ymul * -fy * tz2 * dJ12;
         const float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * Pc.t[0]) * tz3 * dJ02 +
@@ -1490,15 +1264,10 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
         dmean[2] += Vw[8] * dtx + Vw[9] * dty + Vw[10] * dtz;
         // ---- perspective-divide backward
         float hom[4];
-#if LGM_PREPROC_FAST
         hom[0] = Pm[0] * g[0] + Pm[4] * g[1] + Pm[8] * g[2] + Pm[12];
         hom[1] = Pm[1] * g[0] + Pm[5] * g[1] + Pm[9] * g[2] + Pm[13];
         hom[3] = Pm[3] * g[0] + Pm[7] * g[1] + Pm[11] * g[2] + Pm[15];
         const float m_w = __builtin_amdgcn_rcpf(hom[3] + 0.0000001f);
-#else
-        xf44(Pm, g[0], g[1], g[2], hom);
-        const float m_w = 1.0f / (hom[3] + 0.0000001f);
-#endif
         const float mul1 = hom[0] * m_w * m_w;
         const float mul2 = hom[1] * m_w * m_w;
         dmean[0] += (Pm[0] * m_w - Pm[3] * mul1) * dm2x + (Pm[1] * m_w - Pm[3] * mul2) * dm2y;
@@ -1516,11 +1285,6 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
             dop = (float)ldexp((double)a[0], -det_s);
 #pragma unroll
             for (int q = 0; q < 3; q++) dcol[q] = (float)ldexp((double)a[1 + q], -det_s);
-        } else if (LGM_ACC_F64) {
-            const double2 *a = reinterpret_cast<const double2 *>(reinterpret_cast<const double *>(accum) + ks);
-            const double2 a0 = a[0], a1 = a[1];
-            dop = (float)a0.x;
-            dcol[0] = (float)a0.y; dcol[1] = (float)a1.x; dcol[2] = (float)a1.y;
         } else {
             const float4 a = *reinterpret_cast<const float4 *>(accum + ks);
             dop = a.x;
@@ -1557,8 +1321,10 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
     const float out[14] = {dmean[0], dmean[1], dmean[2], dop, dscale[0], dscale[1], dscale[2],
                            dq[0], dq[1], dq[2], dq[3], dcol[0], dcol[1], dcol[2]};
     float2 *o2 = reinterpret_cast<float2 *>(o);
+    const float qnan = __builtin_nanf("");
 #pragma unroll
-    for (int kk = 0; kk < 7; kk++) o2[kk] = make_float2(out[2 * kk], out[2 * kk + 1]);
+    for (int kk = 0; kk < 7; kk++)
+        o2[kk] = det_bad ? make_float2(qnan, qnan) : make_float2(out[2 * kk], out[2 * kk + 1]);
     if (stamp) d.counters[8 + 8 * g_diag + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -1569,7 +1335,7 @@ int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, fl
                       float *alpha, char *ws, const Layout &L, hipStream_t st) {
     auto fwd = (d.options & LGM_RENDER_FUSED_LOSS) ? k_render_fwd<true> : k_render_fwd<false>;
     LGM_LAUNCH("k_render_fwd", st, (fwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
-                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
+                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
                                        image, depth, alpha,
@@ -1595,9 +1361,9 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
     // the per-view accumulators were zeroed by the forward's binning; a repeated backward of the same forward
     // clears what the previous one left
     if ((d.options & LGM_RENDER_BACKWARD_AGAIN) &&
-        hipMemsetAsync(ws + L.accum, 0, (LGM_ACC_F64 || (d.options & LGM_RENDER_DETERMINISTIC))
+        hipMemsetAsync(ws + L.accum, 0, (d.options & LGM_RENDER_DETERMINISTIC)
                                             ? acc_elems(d.B, d.V, d.N) * 8
-                                            : acc_side_offset(d.B, d.V, d.N) * 4 + (ACC_SIDE ? (size_t)d.BV * d.N * 24 : 0),
+                                            : acc_side_offset(d.B, d.V, d.N) * 4 + (size_t)d.BV * d.N * 24,
                        st) != hipSuccess) {
         set_error("hipMemsetAsync failed");
         return LGM_E_HIP;
@@ -1623,9 +1389,9 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
     };
     auto bwd = d_depth ? pick(std::true_type{}) : pick(std::false_type{});
     // work items: chunk 0 of every tile, then one per checkpoint slot (unused slots exit at once)
-    const int M = d.BV * d.T, Mp = LGM_XCD_ORDER ? round8(M) : M;
+    const int M = d.BV * d.T, Mp = round8(M);
     LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(Mp + L.ck_slots), 256, 0, st>>>(
-                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.order), (const int *)(ws + L.tile_start),
+                                       d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,
                                        (const float *)(ws + L.final_T), (const int *)(ws + L.n_contrib),
@@ -1633,6 +1399,7 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
                                        (const int2 *)(ws + L.cklist), (const int *)(ws + L.nck),
                                        (const unsigned *)(ws + L.misc) + 4, L.ck_region, d_image, d_depth, d_alpha,
                                        (const unsigned char *)(ws + L.cmask), (float *)(ws + L.accum), det_max,
+                                       (unsigned *)(ws + L.misc) + 13,
                                        // (debug counters: after the per-tile and per-binning-workgroup records)
                                        8 + 8LL * d.BV * d.T + 8LL * d.BV * ((d.N + 511) / 512))));
     dim3 grid((d.N + 255) / 256, d.B);
@@ -1640,7 +1407,8 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
                                                                         (const uint2 *)(ws + L.rects),
                                                                         (float *)(ws + L.accum), d_gaussians,
                                                                         d_means2D, (const float4 *)(ws + L.gP),
-                                                                        (const float4 *)(ws + L.gQ), det_max)));
+                                                                        (const float4 *)(ws + L.gQ), det_max,
+                                                                        (const unsigned *)(ws + L.misc) + 13)));
     return LGM_OK;
 }
 

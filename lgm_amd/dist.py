@@ -145,6 +145,34 @@ def make_ddp(module, device=None, bucket_cap_mb: float = 100.0, bf16_compress: b
     return ddp
 
 
+class GradAccumulator:
+    """Gradient accumulation over `steps` micro-batches for a make_ddp model, with accelerate's semantics
+    (main.py:93 `accelerator.accumulate(model)`, core/options.py:48 gradient_accumulation_steps): the first
+    steps - 1 micro-steps run their backward inside DDP's no_sync() (gradients summed locally, no all-reduce), the
+    last one all-reduces the summed gradients once; backward() scales the loss by 1 / steps (accelerate.backward)
+    and `sync_gradients` says when the clip and the optimizer step apply (accelerate skips both otherwise).
+        acc = GradAccumulator(ddp, steps)
+        for batch in data:
+            with acc.accumulate():
+                loss = ...; acc.backward(loss)
+                if acc.sync_gradients: clip; opt.step(); opt.zero_grad()"""
+
+    def __init__(self, model, steps: int = 1):
+        if steps < 1:
+            raise ValueError("gradient accumulation steps must be >= 1")
+        self.model, self.steps, self.count, self.sync_gradients = model, int(steps), 0, True
+
+    def accumulate(self):
+        import contextlib
+        self.count += 1
+        self.sync_gradients = self.count % self.steps == 0
+        no_sync = getattr(self.model, "no_sync", None)
+        return contextlib.nullcontext() if self.sync_gradients or no_sync is None else no_sync()
+
+    def backward(self, loss):
+        (loss / self.steps if self.steps > 1 else loss).backward()
+
+
 def allreduce_bucketed(flat, bucket_elems: int, info: RankInfo, bf16: bool = False):
     """All-reduce (average) of one flat fp32 gradient buffer in buckets, as DDP does at the end of the backward:
     the communication cost of the training step's parameter gradients (bench.py's cfg5 object). fp32 on the wire

@@ -207,12 +207,13 @@ def count_pairs(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scal
 
 
 def forward_state(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, scale_modifier=1.0, lists=False,
-                  no_cull=False):
+                  no_cull=False, records=False):
     """Runs one forward and returns what it left in its workspace (numpy, one host sync), for parity tests and
     debugging -- the equivalent of reading upstream's saved buffers (radii, point_list/ranges, n_contrib):
       radii [B,V,N] int32; K_binned / K_reference (as count_pairs); tile_counts [B,V,T] int32;
       n_contrib, final_T [B,V,H,W]; with lists=True, ids[b][v] = the view's tile lists concatenated (tile-major,
-      each in compositing order). no_cull=True bins upstream's full 3-sigma rects (LGM_RENDER_NO_CULL)."""
+      each in compositing order); with records=True, the compositing records P, Q [B,V,N,4] and rects [B,V,N,2]
+      (uint32) of lgm_render_records. no_cull=True bins upstream's full 3-sigma rects (LGM_RENDER_NO_CULL)."""
     options = _native.RENDER_NO_CULL if no_cull else 0
     L = _native.lib()
     g = gaussians.float().contiguous()
@@ -258,6 +259,14 @@ def forward_state(gaussians, cam_view, cam_view_proj, tanfovx, tanfovy, H, W, sc
         per_view = c64.view(B * V, T).sum(1).tolist()
         bounds = np.concatenate([[0], np.cumsum(per_view)])
         out["ids"] = [[flat[bounds[b * V + v]:bounds[b * V + v + 1]] for v in range(V)] for b in range(B)]
+    if records:
+        P = torch.empty(B, V, N, 4, device=dev)
+        Q = torch.empty(B, V, N, 4, device=dev)
+        rects = torch.empty(B, V, N, 2, dtype=torch.int32, device=dev)
+        _native.check(L.lgm_render_records(B, V, N, H, W, _native.ptr(ws), ws_bytes, 0, _native.ptr(P), _native.ptr(Q),
+                                           _native.ptr(rects), stream), "lgm_render_records")
+        out["P"], out["Q"] = P.cpu().numpy(), Q.cpu().numpy()
+        out["rects"] = rects.cpu().numpy().view(np.uint32)
     return out
 
 

@@ -4,6 +4,13 @@ core/attention.py:16-28, 51-64) and core/unet.py MVAttention (:11-49). fp32, CPU
 
 Each case stores: x, upstream grad gy, the module's state_dict (same parameter names as ours), y, dx, and the
 parameter gradients. Regenerate with: PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_attn_golden.py
+
+LGM's real widths (core/unet.py:35-49 with 16 heads, core/unet.py:113-206): C = 512 (D = 32) at 4 views x 32^2
+(L = 4096, the heaviest 'big' level) and C = 1024 (D = 64) at 4 views x 8^2. Their parameters and inputs would be
+tens of MB as arrays, so these "seeded" fixtures store no inputs at all: the parameters, x and gy are drawn from
+a CPU torch.Generator (seed = crc32 of the case name) in a fixed order that tests/test_attention.py replays
+(seeded_inputs), and of every output (y, dx, each parameter gradient) only a deterministic strided sample of at
+most 32,768 elements plus the full array's float64 L2 norm and sum are kept.
 """
 import os
 import sys
@@ -14,6 +21,28 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = "/root/reference"
+
+
+def seeded_inputs(name, param_shapes, x_shape):
+    """The seeded fixtures' inputs, drawn in this order from one CPU generator: every parameter (named_parameters()
+    order; weights * 0.5 / sqrt(fan_in), vectors * 0.1, the GroupNorm weight + 1), then x, then (returned as a
+    function of y's shape) gy. Shared verbatim with tests/test_attention.py, which imports it."""
+    g = torch.Generator().manual_seed(zlib.crc32(name.encode()))
+    params = {}
+    for k, shp in param_shapes:
+        t = torch.randn(shp, generator=g) * (0.5 / np.sqrt(shp[-1]) if len(shp) > 1 else 0.1)
+        if k == "norm.weight":
+            t = t + 1.0
+        params[k] = t
+    x = torch.randn(x_shape, generator=g)
+    return params, x, lambda shape: torch.randn(shape, generator=g)
+
+
+def sample(a, n=32768):
+    """A deterministic strided sample of at most n elements of a flattened array: (indices, values)."""
+    flat = a.reshape(-1)
+    idx = (np.arange(min(n, flat.size), dtype=np.int64) * 7919 + 13) % flat.size
+    return idx.astype(np.int64), flat[idx]
 
 
 def main():
@@ -39,7 +68,35 @@ def main():
         ("mv_c128_h2_f6_l2400", "mv", dict(dim=128, num_heads=2, num_frames=6, skip_scale=0.5 ** 0.5),
          (6, 128, 20, 20)),
     ]
+    seeded = [  # name, ctor kwargs, input shape: LGM's real channel widths, 16 heads
+        ("mv_c512_h16_f4_l4096", dict(dim=512, num_heads=16, num_frames=4, skip_scale=0.5 ** 0.5), (4, 512, 32, 32)),
+        ("mv_c1024_h16_f4_l256", dict(dim=1024, num_heads=16, num_frames=4, skip_scale=0.5 ** 0.5), (4, 1024, 8, 8)),
+    ]
     only = set(sys.argv[1:])  # optional: regenerate only the named cases
+    for name, kw, shape in seeded:
+        if only and name not in only:
+            continue
+        m = MVAttention(kw["dim"], kw["num_heads"], num_frames=kw["num_frames"], skip_scale=kw["skip_scale"])
+        names = [k for k, _ in m.named_parameters()]
+        params, x, draw_gy = seeded_inputs(name, [(k, tuple(p.shape)) for k, p in m.named_parameters()], shape)
+        with torch.no_grad():
+            for k, p in m.named_parameters():
+                p.copy_(params[k])
+        x.requires_grad_(True)
+        y = m(x)
+        gy = draw_gy(y.shape)
+        y.backward(gy)
+        out = {}
+        for k, t in [("y", y.detach()), ("dx", x.grad)] + [("grad." + k, p.grad) for k, p in m.named_parameters()]:
+            a = t.numpy().astype(np.float32)
+            out["idx." + k], out["sample." + k] = sample(a)
+            out["norm." + k] = np.float64(np.linalg.norm(a.astype(np.float64)))
+            out["sum." + k] = np.float64(a.astype(np.float64).sum())
+        meta = dict(kind="mv", seeded=True, shape=shape, params=[(k, tuple(p.shape)) for k, p in m.named_parameters()],
+                    **kw)
+        assert names == [k for k, _ in meta["params"]]
+        np.savez_compressed(os.path.join(HERE, f"attn_{name}.npz"), meta=np.array(repr(meta)), **out)
+        print(name, {k: v.shape for k, v in out.items()})
     for name, kind, kw, shape in cases:
         if only and name not in only:
             continue

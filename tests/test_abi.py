@@ -50,7 +50,7 @@ def test_no_process_wide_switches():
     """no global mutable state besides the error string. The round-2 process-wide setters
     (lgm_render_set_flags, lgm_render_debug_counters, lgm_profiler_attach) are gone: NO_CULL is a per-call option
     bit and diagnostics a per-call lgm_diag; every compute entry point that takes a stream takes a diag after it
-    (the two workspace-inspection copies excepted)."""
+    (the three workspace-inspection copies excepted)."""
     from lgm_amd import build as B
     B.build()
     L = ctypes.CDLL(_native.LIB_PATH)
@@ -59,5 +59,6 @@ def test_no_process_wide_switches():
     for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
         txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
         for name, args in re.findall(r"\b(lgm_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", txt):
-            if "void *stream" in args and name not in ("lgm_render_tile_lists", "lgm_render_pixel_state"):
+            if "void *stream" in args and name not in ("lgm_render_tile_lists", "lgm_render_pixel_state",
+                                                              "lgm_render_records"):
                 assert args.rstrip().endswith("const lgm_diag *diag"), name

@@ -2,7 +2,8 @@
 (lgm_amd.cameras.render_orbit_frames) against the reference's per-frame loop restated line by line (numpy
 orbit_camera -> flip -> torch.inverse -> transpose -> @ proj -> render(V = 1) -> (image * 255).astype(uint8)) on
 the same HIP renderer: bit for bit on the loop's own camera matrices; with the device-built cameras (closed-form
-rigid inverse vs torch.inverse: last-bit differences) within a pixel budget."""
+rigid inverse vs torch.inverse: last-bit differences) within the per-pixel spread that a 1-ulp nudge of the
+loop's own recipe, evaluated exactly and rounded once, produces."""
 import numpy as np
 import pytest
 import torch
@@ -38,11 +39,31 @@ def _reference_loop(renderer, gaussians, cams, scales):
     return np.concatenate(images, axis=0)
 
 
+def _exact_cameras(renderer, azimuths, radius, dev):
+    """The loop's recipe evaluated exactly and rounded once: the same float32 poses, inverted (and multiplied by
+    proj) in float64, then rounded to float32 -- a different, equally valid (more accurate) set of matrices than the
+    loop's float32 torch.inverse."""
+    opt = renderer.opt
+    proj = projection_matrix(opt.fovy, opt.znear, opt.zfar).double()
+    cams = []
+    for azi in azimuths:
+        cam_poses = torch.from_numpy(orbit_camera(0, azi, radius=radius, opengl=True)).unsqueeze(0)
+        cam_poses[:, :3, 1:3] *= -1
+        cam_view = torch.inverse(cam_poses.double()).transpose(1, 2)
+        cams.append(((cam_view.float()).to(dev), (cam_view @ proj).float().to(dev), (-cam_poses[:, :3, 3]).to(dev)))
+    return cams
+
+
 @pytest.mark.parametrize("fancy", [False, True])
 def test_orbit_video_batched_matches_per_frame_loop(cuda, fancy):
-    """Batched (up to 60 views a call) == the per-frame loop bit for bit on the loop's own cameras; with the
-    device-built cameras (last-bit differences in the matrices) the frames agree up to the renderer's
-    discontinuities (a 1/255 alpha threshold or a tile rect edge crossed by a rounding): a pixel budget."""
+    """Batched (up to 60 views a call) == the per-frame loop bit for bit on the loop's own cameras. The device-built
+    cameras are the recipe's exact matrices rounded once (orbit_cameras_batched), which differ from the loop's
+    float32 torch.inverse in the last bits, and the render is discontinuous in its camera: a Gaussian whose alpha
+    sits at the 1/255 threshold, whose transmittance crosses 1e-4, or whose 3-sigma rect touches a tile edge,
+    switches on or off under a 1-ulp change, and the pixels it covers jump by its whole contribution (round 3
+    measured up to 10/255). So the per-pixel bound is calibrated on the reference loop itself: the device cameras
+    may move pixels no more than the loop's own recipe evaluated exactly and rounded once does (max level
+    difference; pixels off by more than 2 levels within 1.5x), and at most 1e-3 of the pixels may differ."""
     renderer = GaussianRenderer(Options(output_size=256))
     g = synthetic_gaussians(1, 30_000, seed=12).to(cuda)
     if fancy:  # infer.py:116-131: azimuths 0..716 step 4, scale_modifier min(azi / 360, 1)
@@ -62,21 +83,37 @@ def test_orbit_video_batched_matches_per_frame_loop(cuda, fancy):
     got = render_orbit_frames(renderer, g, torch.from_numpy(az.astype(np.float32)), radius=1.5,
                               scale_modifier=sm).cpu().numpy()
     diff = np.abs(got.astype(np.int32) - ref.astype(np.int32))
-    frac = float((diff > 0).mean())
-    print(f"fancy={fancy}: device cameras: {frac:.2e} of the frame pixels differ, max {diff.max()}, "
-          f"mean {diff.mean():.2e}")
-    assert frac < 1e-3 and diff.mean() < 1e-3, (frac, int(diff.max()))
+    # the reference loop's own sensitivity: its recipe evaluated exactly and rounded once (what the device builds)
+    exact = _reference_loop(renderer, g, _exact_cameras(renderer, az, 1.5, cuda), scales)
+    dx = np.abs(exact.astype(np.int32) - ref.astype(np.int32))
+    frac, big = float((diff > 0).mean()), float((diff > 2).mean())
+    x_max, x_big = int(dx.max()), float((dx > 2).mean())
+    print(f"fancy={fancy}: device cameras: {frac:.2e} of the frame pixels differ, {big:.2e} by > 2 levels, max "
+          f"{diff.max()}; exactly-rounded recipe cameras: max {x_max}, {x_big:.2e} by > 2 levels")
+    assert frac < 1e-3, frac
+    assert diff.max() <= max(2, x_max), (int(diff.max()), x_max)
+    assert big <= max(1e-6, 1.5 * x_big), (big, x_big)
 
 
 def test_device_cameras_match_reference_recipe(cuda):
-    """orbit_cameras_batched (device, closed form) vs the per-frame recipe's matrices."""
+    """orbit_cameras_batched (device, float64 then one rounding) vs the per-frame recipe evaluated exactly and
+    rounded once, at all 180 azimuths: within 1 float32 ulp on every entry above 1e-6 in magnitude, within 1e-12 on
+    the (exactly zero in exact arithmetic) entries below it."""
     az = np.arange(0, 360, 2, dtype=np.float32)
     cv, cvp, cp = orbit_cameras_batched(0.0, torch.from_numpy(az), 1.5, device=cuda)
-    proj = projection_matrix(49.1, 0.5, 2.5)
-    for i in (0, 17, 45, 90, 179):
+    proj = projection_matrix(49.1, 0.5, 2.5).double()
+
+    def check(got, want):
+        got, want = got.cpu().numpy().astype(np.float32), want.numpy().astype(np.float32)
+        big = np.abs(want) > 1e-6
+        ulp = np.abs(got.view(np.int32).astype(np.int64) - want.view(np.int32).astype(np.int64))
+        assert ulp[big].max(initial=0) <= 1, ulp[big].max()
+        assert np.abs(got - want)[~big].max(initial=0.0) <= 1e-12
+
+    for i in range(len(az)):
         pose = torch.from_numpy(orbit_camera(0, float(az[i]), radius=1.5, opengl=True)).unsqueeze(0)
         pose[:, :3, 1:3] *= -1
         v = torch.inverse(pose.double()).transpose(1, 2)
-        torch.testing.assert_close(cv[i].double().cpu(), v[0], rtol=0, atol=1e-6)
-        torch.testing.assert_close(cvp[i].double().cpu(), (v @ proj.double())[0], rtol=0, atol=2e-6)
-        torch.testing.assert_close(cp[i].double().cpu(), -pose[0, :3, 3].double(), rtol=0, atol=1e-6)
+        check(cv[i], v[0].float())
+        check(cvp[i], (v @ proj)[0].float())
+        check(cp[i], -pose[0, :3, 3])

@@ -142,6 +142,59 @@ def test_make_ddp_buckets(tmp_path, bf16):
     np.testing.assert_allclose(res[0]["flat"], np.mean(flats, 0), rtol=1e-6, atol=1e-6)
 
 
+def _accum_target(tmp):
+    """Two ranks, gloo: 3 micro-steps of gradient accumulation (GradAccumulator) through make_ddp, with a comm hook
+    counting the buckets DDP all-reduces."""
+    info = D.rank_info()
+    D.init("gloo", info)
+    try:
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 14))
+        ddp = D.make_ddp(m, bucket_cap_mb=0.001)
+        calls = []
+
+        def hook(state, bucket):
+            calls.append(len(calls))
+            return torch.distributed.algorithms.ddp_comm_hooks.default_hooks.allreduce_hook(None, bucket)
+
+        ddp.register_comm_hook(None, hook)
+        acc = D.GradAccumulator(ddp, 3)
+        syncs, per_step = [], []
+        for k in range(3):
+            x = torch.randn(5, 16, generator=torch.Generator().manual_seed(100 * info.rank + k))
+            with acc.accumulate():
+                acc.backward(ddp(x).pow(2).sum())
+                syncs.append(acc.sync_gradients)
+                per_step.append(len(calls))
+        np.savez(os.path.join(tmp, f"a{info.rank}.npz"), g=np.concatenate([p.grad.numpy().ravel() for p in m.parameters()]),
+                 syncs=np.array(syncs), calls=np.array(per_step))
+    finally:
+        D.finalize(info)
+
+
+def test_gradient_accumulation_no_sync(tmp_path):
+    """accelerate.accumulate's DDP path (main.py:93, gradient_accumulation_steps) through GradAccumulator: the first
+    micro-steps all-reduce nothing (no_sync), the last all-reduces once, and every rank ends with the mean over ranks
+    of the per-rank sums of loss / steps gradients."""
+    D.spawn_ranks(_accum_target, WORLD, str(tmp_path))
+    res = [np.load(os.path.join(tmp_path, f"a{r}.npz")) for r in range(WORLD)]
+    np.testing.assert_array_equal(res[0]["g"], res[1]["g"])
+    for r in res:
+        assert r["syncs"].tolist() == [False, False, True]
+        assert r["calls"][0] == 0 and r["calls"][1] == 0 and r["calls"][2] > 0
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 14))
+    grads = []
+    for r in range(WORLD):
+        m.zero_grad()
+        for k in range(3):
+            x = torch.randn(5, 16, generator=torch.Generator().manual_seed(100 * r + k))
+            (m(x).pow(2).sum() / 3).backward()
+        grads.append(np.concatenate([p.grad.numpy().ravel() for p in m.parameters()]))
+    mean = np.mean(grads, 0)
+    assert np.abs(res[0]["g"] - mean).max() <= 1e-6 * np.abs(mean).max()
+
+
 def test_shard_range():
     for n in range(0, 20):
         for w in range(1, 9):

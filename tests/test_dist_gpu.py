@@ -208,3 +208,66 @@ def test_make_ddp_rccl_single_rank(cuda, tmp_path, monkeypatch, bf16):
     for i, p in enumerate(model.parameters()):
         ref = p.detach().cpu().numpy()
         np.testing.assert_allclose(z[f"p_{i}"], ref, rtol=0, atol=(1e-3 if bf16 else 1e-6) * np.abs(ref).max())
+
+
+def _accum_worker(tmp):
+    """make_ddp + GradAccumulator (2 micro-steps, accelerate.accumulate's path) on a real one-rank RCCL group: the
+    first micro-step's backward runs under no_sync, the second all-reduces the summed gradients; then the clip and
+    AdamW step of main.py:99-109."""
+    import torch.distributed as dist
+    os.environ["LGM_AMD_DETERMINISTIC"] = "1"
+    torch.backends.cudnn.deterministic = True
+    info = D.rank_info()
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=info.rank, world_size=info.world, device_id=dev)
+    try:
+        torch.manual_seed(3)
+        model = _TinyLGM().to(dev)
+        ddp = D.make_ddp(model, device=dev)
+        opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3)
+        images, cams, gt, mask, bg, renderer = _ddp_inputs(dev)
+        acc = D.GradAccumulator(ddp, 2)
+        syncs = []
+        for k in range(2):
+            with acc.accumulate():
+                out = renderer.render(ddp(images * (1.0 + 0.25 * k)), *cams, bg_color=bg, gt_images=gt, gt_masks=mask)
+                acc.backward(out["loss_mse"])
+                syncs.append(acc.sync_gradients)
+                if acc.sync_gradients:
+                    torch.nn.utils.clip_grad_norm_(ddp.parameters(), 1.0)
+                    grads = [p.grad.detach().clone() for p in model.parameters()]
+                    opt.step()
+                    opt.zero_grad()
+        torch.cuda.synchronize()
+        np.savez(os.path.join(tmp, "acc.npz"), syncs=np.array(syncs),
+                 **{f"g_{i}": t.cpu().numpy() for i, t in enumerate(grads)},
+                 **{f"p_{i}": p.detach().cpu().numpy() for i, p in enumerate(model.parameters())})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradient_accumulation_rccl_single_rank(cuda, tmp_path, monkeypatch):
+    """Gradient accumulation through DDP on RCCL (GradAccumulator: no_sync micro-step, then one all-reduce) equals
+    the accumulated plain step: the summed gradients of loss / 2 over both micro-batches (fp32 rounding; the render
+    and head gradients are deterministic), and the parameters after the clip and AdamW step."""
+    D.spawn_ranks(_accum_worker, 1, str(tmp_path))
+    z = np.load(os.path.join(tmp_path, "acc.npz"))
+    assert z["syncs"].tolist() == [False, True]
+    monkeypatch.setenv("LGM_AMD_DETERMINISTIC", "1")
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    torch.manual_seed(3)
+    model = _TinyLGM().to(cuda)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    images, cams, gt, mask, bg, renderer = _ddp_inputs(cuda)
+    for k in range(2):
+        out = renderer.render(model(images * (1.0 + 0.25 * k)), *cams, bg_color=bg, gt_images=gt, gt_masks=mask)
+        (out["loss_mse"] / 2).backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+    for i, p in enumerate(model.parameters()):
+        ref = p.grad.cpu().numpy()
+        np.testing.assert_allclose(z[f"g_{i}"], ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+    opt.step()
+    for i, p in enumerate(model.parameters()):
+        ref = p.detach().cpu().numpy()
+        np.testing.assert_allclose(z[f"p_{i}"], ref, rtol=0, atol=1e-6 * np.abs(ref).max())

@@ -3,7 +3,7 @@
 Tolerances (north_star, BASELINE.json: "within 1e-4 rel L2 (fp32)"):
   * forward outputs (image, depth, alpha): relative L2 < 1e-4 against the fp32 oracle;
   * gradients dL/dgaussians, per parameter group: relative L2 against the SAME algorithm evaluated in fp64
-    (oracle built with -DLGM_ORACLE_F64) must not exceed max(1e-4, 2 x the fp32 oracle's own error against
+    (oracle built with -DLGM_ORACLE_F64) must not exceed max(1e-4, 1.25 x the fp32 oracle's own error against
     fp64). Rationale: a few ill-conditioned Gaussians (needles, near-clamped) make the rotation/scale gradients
     fp32-noise-limited -- at cfg3 the faithful fp32 restatement itself is 1.9e-4 (d_rot) and 1.0e-4 (d_scale)
     away from fp64, so 1e-4 between two fp32 implementations is below the algorithm's own noise floor there;
@@ -15,7 +15,7 @@ import torch
 
 from lgm_amd import gs as lgs
 from lgm_amd.gs import rasterize
-from tests.render_cases import TAN, rel_l2, scene, upstream
+from tests.render_cases import TAN, grad_bar, rel_l2, scene, upstream
 
 pytestmark = pytest.mark.gpu
 
@@ -60,7 +60,7 @@ def _check_bwd(out, ref, tol=BWD_TOL):
     for name, sl in GROUPS.items():
         e_gpu = rel_l2(out["d_gaussians"][..., sl], truth[..., sl])
         e_o32 = rel_l2(ref["d_gaussians"][..., sl], truth[..., sl])
-        assert e_gpu < max(tol, 2.0 * e_o32), f"d_{name}: GPU vs fp64 {e_gpu:.3e}, fp32 oracle vs fp64 {e_o32:.3e}"
+        assert e_gpu < grad_bar(e_o32, tol), f"d_{name}: GPU vs fp64 {e_gpu:.3e}, fp32 oracle vs fp64 {e_o32:.3e}"
 
 
 @pytest.mark.parametrize("B,N,V,H,W,mod", [(1, 1, 1, 32, 32, 1.0), (1, 300, 2, 64, 64, 1.0), (2, 2000, 3, 64, 64, 1.0),
@@ -226,3 +226,34 @@ def test_fused_clamp_matches_torch_clamp(cuda):
     assert 0.01 < frac < 0.9, frac  # the clamp is actually exercised
     assert torch.equal(outs[True][0], raw.clamp(0, 1))
     assert rel_l2(outs[True][1].cpu().numpy(), outs[False][1].cpu().numpy()) < 1e-5
+
+
+def test_needle_flag_is_a_function_of_the_stored_record(cuda):
+    """Float mode sends a needle-like record's conic partials to fp64 side accumulators; the binning flags the record
+    (bit 31 of its rect, read by the preprocess backward) from the record in registers, the backward's flush
+    re-derives the flag from the record loaded back from memory (render_common.h rec_needle). They agree only if
+    the decision is a pure function of the stored bits: FP contraction off, separately rounded IEEE operations.
+    Checked on every visible record of cfg4's 512^2 needle-heavy scene (5 views): the binning's flag equals the
+    same expression evaluated in float32 by numpy on the stored (A', B', C'), including the records nearest the
+    threshold (condition 300)."""
+    from lgm_amd.gs import forward_state
+    from lgm_amd.synthetic import synthetic_gaussians
+    from lgm_amd.cameras import orbit_cameras
+    g = synthetic_gaussians(1, 153_600, seed=4)
+    cv, cvp, _ = orbit_cameras(20)
+    cv, cvp = cv[None, 0:20:4].contiguous(), cvp[None, 0:20:4].contiguous()
+    st = forward_state(g.to(cuda), cv.to(cuda), cvp.to(cuda), TAN, TAN, 512, 512, records=True)
+    P, Q, rects = st["P"].reshape(-1, 4), st["Q"].reshape(-1, 4), st["rects"].reshape(-1, 2)
+    vis = (rects[:, 0] & 0xFFFF) != (rects[:, 1] & 0xFFFF)
+    Ap, Bp, Cp = P[vis, 2], P[vis, 3], Q[vis, 0]
+    f32 = np.float32
+    sac = (Ap + Cp).astype(f32)
+    dq = (Ap * Cp).astype(f32) - ((f32(0.25) * Bp).astype(f32) * Bp).astype(f32)
+    with np.errstate(invalid="ignore", over="ignore"):
+        needle = ~((sac * sac).astype(f32) <= (f32(300.0) * dq).astype(f32))
+        flag = (rects[vis, 1] >> 31).astype(bool)
+        cond = (sac.astype(np.float64) ** 2) / dq.astype(np.float64)
+    near = np.sort(np.abs(cond[np.isfinite(cond) & (dq > 0)] / 300.0 - 1.0))[:5]
+    print(f"{int(vis.sum())} visible records, {int(needle.sum())} needles; nearest |cond/300 - 1|: {near}")
+    assert needle.sum() > 0
+    assert np.array_equal(flag, needle), f"{int((flag != needle).sum())} records flagged differently"

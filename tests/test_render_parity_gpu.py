@@ -13,7 +13,8 @@ tile's sorted id list and every pixel's n_contrib equal the oracle's. With culli
 oracle's list with the provably-skipped pairs removed, in the same order.
 
 Tolerances for floats are those of tests/test_render_gpu.py (forward 1e-4 rel L2; gradients within
-max(1e-4, 2 x the fp32 oracle's own error) of fp64).
+max(1e-4, 1.25 x the fp32 oracle's own error) of fp64; the GPU's distance to the fp32 oracle itself is
+recorded beside it).
 """
 import glob
 import os
@@ -26,7 +27,7 @@ from lgm_amd import GaussianRenderer, Options, _native
 from lgm_amd.gs import forward_state
 from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads
 from lgm_amd.cameras import orbit_cameras
-from tests.render_cases import PRECISION, TAN, rel_l2, scene, upstream
+from tests.render_cases import PRECISION, TAN, grad_bar, rel_l2, scene, upstream
 
 pytestmark = pytest.mark.gpu
 
@@ -76,7 +77,8 @@ def _check(O, out, g, cv, cvp, H, W, bg, d_img_masked, d_alpha, mod=1.0, name=No
     for grp, sl in GROUPS.items():
         e_gpu = rel_l2(out["d_gaussians"][..., sl], truth[..., sl])
         e_o32 = rel_l2(ref["d_gaussians"][..., sl], truth[..., sl])
-        rec[grp] = {"gpu": e_gpu, "fp32_oracle": e_o32, "bar": max(BWD_TOL, 2.0 * e_o32)}
+        rec[grp] = {"gpu": e_gpu, "fp32_oracle": e_o32, "bar": grad_bar(e_o32, BWD_TOL),
+                    "gpu_vs_fp32_oracle": rel_l2(out["d_gaussians"][..., sl], ref["d_gaussians"][..., sl])}
     if name:
         PRECISION.append({"test": name, "groups": rec})
     for grp, r in rec.items():
@@ -131,7 +133,7 @@ def test_production_cfg4_512(cuda, oracle_mod):
 @pytest.mark.parametrize("path", GOLDEN, ids=lambda p: os.path.basename(p)[7:-4])
 def test_golden_fixture(cuda, oracle_mod, path):
     """Each committed fixture (tests/golden/render_*.npz, elevated cameras included): forward vs its stored
-    outputs, gradients (with its stored d_depth) vs its stored fp32 oracle gradient within max(1e-4, 2 x that
+    outputs, gradients (with its stored d_depth) vs its stored fp32 oracle gradient within max(1e-4, 1.25 x that
     gradient's own error against a live fp64 evaluation)."""
     from lgm_amd.gs import rasterize
     z = np.load(path)
@@ -154,7 +156,7 @@ def test_golden_fixture(cuda, oracle_mod, path):
     for name, sl in GROUPS.items():
         e_gpu = rel_l2(dg[..., sl], truth[..., sl])
         e_fix = rel_l2(z["d_gaussians"][..., sl], truth[..., sl])
-        assert e_gpu < max(BWD_TOL, 2.0 * e_fix), f"d_{name}: {e_gpu:.3e} vs fixture {e_fix:.3e}"
+        assert e_gpu < grad_bar(e_fix, BWD_TOL), f"d_{name}: {e_gpu:.3e} vs fixture {e_fix:.3e}"
 
 
 # ---------------------------------------------------------------------------------------------- integer parity
@@ -306,8 +308,8 @@ def test_needles_512_vs_fp32_oracle(cuda, oracle_mod, det):
     by a few needle-like footprints (conic condition 1e3-2e4: the cov2D inverse amplifies any rounding of their conic
     gradients). The backward's moment MFMAs split w / u into round-to-nearest bf16 hi + lo parts (unbiased, <= 2^-17
     per product; the truncated split sat near 2x the oracle's error here, profiles/r03/diag_float_spread):
-    deterministic mode at or below the fp32 oracle's own error vs fp64 in those groups; float atomics (an
-    accumulation-order draw) within the usual bar."""
+    both accumulation modes at or below the fp32 oracle's own error vs fp64 in those groups (measured 0.36-0.44x in
+    both: the float mode's needle conic partials are summed in fp64), the other groups within the usual bar."""
     g = synthetic_gaussians(1, 153_600, seed=4)
     cv, cvp, _ = orbit_cameras(20)
     cv, cvp = cv[None, 0:20:4].contiguous(), cvp[None, 0:20:4].contiguous()
@@ -327,8 +329,9 @@ def test_needles_512_vs_fp32_oracle(cuda, oracle_mod, det):
     for grp, sl in GROUPS.items():
         e_gpu = rel_l2(out["d_gaussians"][..., sl], truth[..., sl])
         e_o32 = rel_l2(ref["d_gaussians"][..., sl], truth[..., sl])
-        rec[grp] = {"gpu": e_gpu, "fp32_oracle": e_o32, "bar": e_o32 if det and grp in ("mean", "scale", "rot")
-                    else max(BWD_TOL, 2.0 * e_o32)}
+        rec[grp] = {"gpu": e_gpu, "fp32_oracle": e_o32, "bar": e_o32 if grp in ("mean", "scale", "rot")
+                    else grad_bar(e_o32, BWD_TOL),
+                    "gpu_vs_fp32_oracle": rel_l2(out["d_gaussians"][..., sl], ref["d_gaussians"][..., sl])}
     PRECISION.append({"test": f"cfg4 512^2, 5 views, needle-dominated ({'deterministic' if det else 'float'} mode)",
                       "groups": rec})
     for grp, r in rec.items():

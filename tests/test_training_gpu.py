@@ -6,7 +6,7 @@ into the kernels, and the backward through both -- with bench.py's exact cfg5 in
   autograd): loss terms 1e-5, dL/dx (the UNet output's gradient) and the conv's gradients 1e-4 rel L2 per group;
 * 4 of the 26 views against the oracle: the GPU's forward vs the fp32 oracle (1e-4), the loss vs the oracle's
   outputs, and dL/dgaussians of the fused loss -- float-atomic AND deterministic mode -- vs the fp64 oracle fed the
-  same MSE seeds, within max(1e-4, 2 x the fp32 oracle's own error); then dL/dx through the head vs the fp64 torch
+  same MSE seeds, within max(1e-4, 1.25 x the fp32 oracle's own error); then dL/dx through the head vs the fp64 torch
   restatement of the head (oracle/head_ref.py) fed the fp64 oracle's dL/dgaussians;
 * deterministic mode at this gradient scale (mean-MSE seeds ~1e-8): bitwise reproducible, and within
   the bar of the float-atomic path.
@@ -17,7 +17,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from tests.render_cases import PRECISION, TAN, rel_l2
+from tests.render_cases import PRECISION, TAN, grad_bar, rel_l2
 
 pytestmark = pytest.mark.gpu
 GROUPS = {"mean": slice(0, 3), "opacity": slice(3, 4), "scale": slice(4, 7), "rot": slice(7, 11), "rgb": slice(11, 14)}
@@ -128,14 +128,16 @@ def test_cfg5_oracle_subset(cfg5, oracle_mod):
     mi = float(np.mean((np.clip(ref64["image"], 0, 1) - gt_c) ** 2))
     ma = float(np.mean((ref64["alpha"] - mask) ** 2))
     assert abs(flo["terms"]["mse_image"] - mi) <= 1e-5 * mi and abs(flo["terms"]["mse_alpha"] - ma) <= 1e-5 * ma
-    # dL/dgaussians, both accumulation modes, vs fp64 (bar: max(1e-4, 2 x the fp32 oracle's own error))
+    # dL/dgaussians, both accumulation modes, vs fp64 (bar: max(1e-4, 1.25 x the fp32 oracle's own error))
     rec = {"test": "cfg5_oracle_subset (4 of 26 views, 512^2, N = 153,600, fused MSE loss)", "groups": {}}
     for name, sl in GROUPS.items():
         e_o32 = rel_l2(ref32["d_gaussians"][..., sl], truth[..., sl])
-        bar = max(1e-4, 2.0 * e_o32)
+        bar = grad_bar(e_o32)
         e_flo = rel_l2(flo["d_g"].cpu().numpy()[..., sl], truth[..., sl])
         e_det = rel_l2(det["d_g"].cpu().numpy()[..., sl], truth[..., sl])
-        rec["groups"][name] = {"bar": bar, "fp32_oracle": e_o32, "gpu_float_atomics": e_flo, "gpu_deterministic": e_det}
+        rec["groups"][name] = {"bar": bar, "fp32_oracle": e_o32, "gpu_float_atomics": e_flo, "gpu_deterministic": e_det,
+                               "gpu_float_vs_fp32_oracle": rel_l2(flo["d_g"].cpu().numpy()[..., sl],
+                                                                  ref32["d_gaussians"][..., sl])}
     PRECISION.append(rec)
     for name, r in rec["groups"].items():
         assert r["gpu_float_atomics"] < r["bar"], (name, r)

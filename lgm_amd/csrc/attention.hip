@@ -443,6 +443,19 @@ __device__ __forceinline__ typename Ty<DT>::V8 tr_frag(const typename Ty<DT>::T 
 // 2-way on both (SQ_LDS_BANK_CONFLICT = half of the forward's LDS cycles, profiles/r02/pmc_attn). Measured
 // (profiles/r02/ab_attn_pad): D = 64 fwd / dQ / dK,dV -5 / -8 / -10 %; D = 32 unchanged.
 constexpr int LDK_PAD = 16, FWD_WPE = 3, BWD_WPE = 2;
+#ifndef LGM_AB_ATT
+#define LGM_AB_ATT 0  // (A/B in progress) 1: -delta folded into the dP MFMA's accumulator; 2: also the exp2 argument's
+                      // scale folded into the register operand and its offset into the S MFMA's accumulator
+#endif
+constexpr float ATT_THR = 8.0f;  // (LGM_AB_ATT 2) forward: the row reference m is raised only when a score exceeds it
+                                 // by more than this (log2 units): P <= 2^8, exact either way
+template <int DT, int N>
+__device__ __forceinline__ void prescale(typename Ty<DT>::V8 (&v)[N], float c) {  // v *= c, rounded to the type
+#pragma unroll
+    for (int a = 0; a < N; a++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[a][j] = (typename Ty<DT>::T)((float)v[a][j] * c);
+}
 constexpr long long QS_MIN_GRID = 512;  // two query sub-tiles per wave once the grid has this many workgroups
 template <int DT, int D, int QS>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FWD_WPE : 1))) void k_attn_fwd2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
@@ -466,13 +479,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
     for (int s = 0; s < QS; s++) {
         const int qr = q0 + 16 * s + r16;
         load_yfrag<DT, D>(qf[s], q + base + (long long)qr * ld, qr < L, g);
+        if (LGM_AB_ATT >= 2) prescale<DT, D / 32>(qf[s].v, c);  // scores come out in log2 units
     }
     f32x4 oacc[QS][D / 16], lacc[QS];
     float m[QS];
 #pragma unroll
     for (int s = 0; s < QS; s++) {
         lacc[s] = zero4();
-        m[s] = -INFINITY;
+        m[s] = LGM_AB_ATT >= 2 ? 0.f : -INFINITY;
 #pragma unroll
         for (int dt = 0; dt < D / 16; dt++) oacc[s][dt] = zero4();
     }
@@ -520,7 +534,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
                 kf[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
 #pragma unroll
             for (int s = 0; s < QS; s++) {
-                f32x4 a = zero4();
+                // (LGM_AB_ATT 2: the accumulator starts at -m, so the MFMA leaves exp2's argument itself)
+                f32x4 a = LGM_AB_ATT >= 2 ? f32x4{-m[s], -m[s], -m[s], -m[s]} : zero4();
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) a = mfma32<DT>(kf[cc], qf[s].v[cc], a);
                 sacc[s][sub] = a;
@@ -537,6 +552,41 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
         }
         // ---- online softmax per query sub-tile; P as the B operand (key order of tr_frag)
         V8 pb[QS][2];
+#if LGM_AB_ATT >= 2
+        // x = score - m (log2 units) straight from the MFMA. The reference m is raised (and O, l rescaled, x
+        // shifted) only on the first tile or where some x exceeds ATT_THR: P = 2^x <= 2^ATT_THR, so no per-tile row
+        // max and no per-score fma
+#pragma unroll
+        for (int s = 0; s < QS; s++) {
+            float mxl = fmaxf(fmaxf(sacc[s][0][0], sacc[s][0][1]), fmaxf(sacc[s][0][2], sacc[s][0][3]));
+#pragma unroll
+            for (int sub = 1; sub < 4; sub++)
+                mxl = fmaxf(fmaxf(mxl, sacc[s][sub][0]), fmaxf(fmaxf(sacc[s][sub][1], sacc[s][sub][2]), sacc[s][sub][3]));
+            if (__ballot(kb == 0 || mxl > ATT_THR)) {  // wave-uniform, rare: kept a branch (not if-converted)
+                asm volatile("" ::: "memory");
+                const float mx = xmax_groups(mxl);
+                const float dlt = kb == 0 ? mx : fmaxf(mx, 0.f);
+                if (kb != 0) {
+                    const float alpha = __builtin_amdgcn_exp2f(-dlt);
+#pragma unroll
+                    for (int dt = 0; dt < D / 16; dt++) oacc[s][dt] *= alpha;
+                    lacc[s] *= alpha;
+                }
+                m[s] += dlt;
+#pragma unroll
+                for (int sub = 0; sub < 4; sub++) sacc[s][sub] -= dlt;
+            }
+#pragma unroll
+            for (int t = 0; t < 2; t++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    pb[s][t][i] = (T)__builtin_amdgcn_exp2f(sacc[s][2 * t][i]);
+                    pb[s][t][4 + i] = (T)__builtin_amdgcn_exp2f(sacc[s][2 * t + 1][i]);
+                }
+#pragma unroll
+            for (int t = 0; t < 2; t++) lacc[s] = mfma32<DT>(ones, pb[s][t], lacc[s]);
+        }
+#else
 #pragma unroll
         for (int s = 0; s < QS; s++) {
             float mx = fmaxf(fmaxf(sacc[s][0][0], sacc[s][0][1]), fmaxf(sacc[s][0][2], sacc[s][0][3]));
@@ -563,6 +613,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
 #pragma unroll
             for (int t = 0; t < 2; t++) lacc[s] = mfma32<DT>(ones, pb[s][t], lacc[s]);
         }
+#endif
         // ---- O^T += V^T P
 #pragma unroll
         for (int t = 0; t < 2; t++)
@@ -590,7 +641,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
             for (int dt = 0; dt < D / 16; dt++)
 #pragma unroll
                 for (int i = 0; i < 4; i++) orow[16 * dt + 4 * g + i] = from_f<T>(oacc[s][dt][i] * inv);
-            if (g == 0) lse[(long long)bh * L + qr] = (m[s] * c + log2f(l)) * LN2;
+            if (g == 0) lse[(long long)bh * L + qr] = ((LGM_AB_ATT >= 2 ? m[s] : m[s] * c) + log2f(l)) * LN2;
         }
     }
 }
@@ -649,6 +700,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         const int kr = k0 + 16 * s + r16;
         load_yfrag<DT, D>(kf[s], k + base + (long long)kr * ld, kr < L, g);
         load_yfrag<DT, D>(vf[s], v + base + (long long)kr * ld, kr < L, g);
+        if (LGM_AB_ATT >= 2) prescale<DT, D / 32>(kf[s].v, c);  // S in log2 units
     }
     f32x4 dka[KS][D / 16], dva[KS][D / 16];
 #pragma unroll
@@ -686,9 +738,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                 qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
                 orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
             }
+            // (LGM_AB_ATT: the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i)
+            f32x4 ainit = zero4(), dinit = zero4();
+            if (LGM_AB_ATT >= 1)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    if (LGM_AB_ATT >= 2) ainit[i] = -sl[cur][16 * sub + 4 * g + i];
+                    dinit[i] = -sd[cur][16 * sub + 4 * g + i];
+                }
 #pragma unroll
             for (int s = 0; s < KS; s++) {
-                f32x4 a = zero4(), dp = zero4();
+                f32x4 a = ainit, dp = dinit;
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
                     a = mfma32<DT>(qr[cc], kf[s].v[cc], a);     // S[q = 16 sub + 4g + i][key]
@@ -707,8 +767,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                 const float l2 = sl[cur][qi], dl = sd[cur][qi];
 #pragma unroll
                 for (int s = 0; s < KS; s++) {
-                    const float p = __builtin_amdgcn_exp2f(fmaf(sacc[s][sub][i], c, -l2));
-                    const float ds = p * (dpa[s][sub][i] - dl);
+                    const float p = __builtin_amdgcn_exp2f(LGM_AB_ATT >= 2 ? sacc[s][sub][i] : fmaf(sacc[s][sub][i], c, -l2));
+                    const float ds = p * (LGM_AB_ATT >= 1 ? dpa[s][sub][i] : dpa[s][sub][i] - dl);
                     pb[s][sub >> 1][4 * (sub & 1) + i] = (T)p;
                     db[s][sub >> 1][4 * (sub & 1) + i] = (T)ds;
                 }
@@ -775,6 +835,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         load_yfrag<DT, D>(of[s], dout + obase + (long long)qr * H * D, qv, g);
         l2[s] = qv ? lse[(long long)bh * L + qr] * LOG2E : INFINITY;
         dl[s] = qv ? delta[(long long)bh * L + qr] : 0.f;
+        if (LGM_AB_ATT >= 2) prescale<DT, D / 32>(qf[s].v, c);  // S in log2 units
     }
     f32x4 dqa[QS][D / 16];
 #pragma unroll
@@ -804,7 +865,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
             }
 #pragma unroll
             for (int s = 0; s < QS; s++) {
-                f32x4 a = zero4(), dp = zero4();
+                // (LGM_AB_ATT: the accumulators start at -lse' / -delta of the lane's query)
+                f32x4 a = LGM_AB_ATT >= 2 ? f32x4{-l2[s], -l2[s], -l2[s], -l2[s]} : zero4();
+                f32x4 dp = LGM_AB_ATT >= 1 ? f32x4{-dl[s], -dl[s], -dl[s], -dl[s]} : zero4();
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
                     a = mfma32<DT>(kr[cc], qf[s].v[cc], a);    // S^T[key = 16 sub + 4g + i][q]
@@ -822,8 +885,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                 const bool kv = !TAIL || kb + 16 * sub + 4 * g + i < L;
 #pragma unroll
                 for (int s = 0; s < QS; s++) {
-                    const float p = kv ? __builtin_amdgcn_exp2f(fmaf(sacc[s][sub][i], c, -l2[s])) : 0.f;
-                    db[s][sub >> 1][4 * (sub & 1) + i] = (T)(p * (dpa[s][sub][i] - dl[s]));
+                    const float p = kv ? __builtin_amdgcn_exp2f(LGM_AB_ATT >= 2 ? sacc[s][sub][i]
+                                                                                : fmaf(sacc[s][sub][i], c, -l2[s]))
+                                       : 0.f;
+                    db[s][sub >> 1][4 * (sub & 1) + i] =
+                        (T)(p * (LGM_AB_ATT >= 1 ? dpa[s][sub][i] : dpa[s][sub][i] - dl[s]));
                 }
             }
 #pragma unroll

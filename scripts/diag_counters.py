@@ -18,7 +18,7 @@ cv, cvp, cp = (t[None].expand(B, *t.shape).contiguous().to(dev) for t in orbit_c
 d_img, _, d_alpha, bg = synthetic_upstream_grads(B, 6, 256, 256, seed=1001 if B == 1 else 1002)
 M = B * 6 * 256
 NB = B * 6 * ((100000 + 511) // 512)  # binning records reserved (k_bin uses the first B*ceil(6/3)*ceil(N/512): 3 views per workgroup)
-NI = 5 * M  # backward work-item capacity
+NI = 12 * M + 256  # backward work-item capacity (the one-wave backward: 4 items per tile and per checkpoint slot)
 cnt = torch.zeros(8 + 8 * M + 8 * NB + 4 * NI, dtype=torch.int64, device=dev)
 L = _native.lib()
 for _ in range(5):  # warm up (clocks, caches, code objects) before the instrumented step
@@ -36,7 +36,7 @@ names = ["fwd_wave_iters", "fwd_contribs", "bwd_wave_iters", "bwd_contribs", "bw
 res = dict(zip(names, c[:8]))
 import numpy as np  # noqa: E402
 tl = np.array(c[8:8 + 8 * M], dtype=np.int64).reshape(M, 8)
-nl = tl[:, 6]
+nl = tl[:, 6] & 0xFFFFFFFF
 res["tile_list_max"] = int(nl.max())
 res["tile_list_p50"] = float(np.median(nl))
 res["tile_list_mean"] = float(nl.mean())

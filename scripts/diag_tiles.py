@@ -26,7 +26,7 @@ with _native.diagnostics(render_counters=cnt):
     r.render(g, cv[None].to(dev), cvp[None].to(dev), cp[None].to(dev))
     torch.cuda.synchronize()
 tl = np.array(cnt[8: 8 + 8 * M].tolist(), dtype=np.int64).reshape(M, 8)
-n, staged = tl[:, 6], tl[:, 7] & 0xFFFFFFFF
+n, staged = tl[:, 6] & 0xFFFFFFFF, tl[:, 7] & 0xFFFFFFFF
 res = {"n_mean": float(n.mean()), "n_max": int(n.max()), "staged_mean": float(staged.mean()),
        "staged_max": int(staged.max()), "frac_consumed": float(staged.sum() / max(1, n.sum()))}
 for K in (256, 512, 768, 1024, 1536, 2048):

@@ -15,7 +15,7 @@ bt = c[8 + 8 * M:8 + 8 * M + 8 * NB].reshape(NB, 8)
 it = c[8 + 8 * M + 8 * NB:].reshape(NI, 4)
 okb = bt[:, 4] > 0
 t0 = bt[okb, 0].min()
-ks = {"bin": (bt[okb, 0], bt[okb, 4], None), "sort": (tl[:, 4], tl[:, 5], tl[:, 6]),
+ks = {"bin": (bt[okb, 0], bt[okb, 4], None), "sort": (tl[:, 4], tl[:, 5], tl[:, 6] & 0xFFFFFFFF),
       "fwd": (tl[:, 0], tl[:, 1], tl[:, 7] & 0xFFFFFFFF)}
 oki = it[:, 1] > 0
 ks["bwd"] = (it[oki, 0], it[oki, 1], it[oki, 2] & 0xFFFFF)
@@ -54,7 +54,7 @@ for name, (st, en, w) in ks.items():
         order = np.argsort(-dur)[:8]
         idx = np.nonzero(ok)[0]
         print(f"{'':12s} longest (tile, staged, steps_w0, dur):",
-              [(int(idx[i]), int(w[ok][i]), int((tl[idx[i], 7] >> 32)), round(float(dur[i]), 1)) for i in order])
+              [(int(idx[i]), int(w[ok][i]), int((tl[idx[i], 7] >> 32) & 0xFFFFFF), round(float(dur[i]), 1)) for i in order])
     if name == "sort":
         order = np.argsort(-en)[:8]
         idx = np.nonzero(ok)[0]

@@ -120,9 +120,10 @@ int lgm_render_records(int B, int V, int N, int H, int W, const void *workspace,
  * [+6] the tile's binned list length, [+7] list entries the forward staged (low 32 bits) and wave 0's
  * 4-entry steps (high 32 bits); then 8 entries per binning workgroup
  * (room for B*V*ceil(N/512); the binning launch uses its first B*ceil(V/3)*ceil(N/512)): phase stamps [0] start,
- * [1] preprocessed, [2] tile tests done, [3] reserved, [4] end, and [5] its binned pairs; then 4 entries per backward
- * work item: start/end stamps, (entries | chunk << 20 | tile << 40) and one unused -- so the buffer must hold
- * 8 + 8*B*V*tiles + 8*B*V*ceil(N/512) + 4*5*B*V*tiles entries. */
+ * [1] preprocessed, [2] tile tests done, [3] reserved, [4] end, [5] its binned pairs, [6] HW_ID and [7] XCC_ID of where it
+ * ran; then 4 entries per backward work item (at most 3*B*V*tiles + 16 items: one per tile, rounded up to 8, and
+ * one per checkpoint slot): start/end stamps, (entries | chunk << 20 | tile << 40) and one unused -- so the buffer
+ * must hold 8 + 8*B*V*tiles + 8*B*V*ceil(N/512) + 4*(3*B*V*tiles + 16) entries. */
 
 /* Per-call `options` of lgm_render_forward / lgm_render_backward (pass the same value to both).
  * LGM_RENDER_CLAMP_IMAGE: the forward writes clamp(image, 0, 1) (core/gs.py:87) and keeps a per-pixel mask in

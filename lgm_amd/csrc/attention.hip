@@ -443,12 +443,12 @@ __device__ __forceinline__ typename Ty<DT>::V8 tr_frag(const typename Ty<DT>::T 
 // 2-way on both (SQ_LDS_BANK_CONFLICT = half of the forward's LDS cycles, profiles/r02/pmc_attn). Measured
 // (profiles/r02/ab_attn_pad): D = 64 fwd / dQ / dK,dV -5 / -8 / -10 %; D = 32 unchanged.
 constexpr int LDK_PAD = 16, FWD_WPE = 3, BWD_WPE = 2;
-#ifndef LGM_AB_ATT
-#define LGM_AB_ATT 0  // (A/B in progress) 1: -delta folded into the dP MFMA's accumulator; 2: also the exp2 argument's
-                      // scale folded into the register operand and its offset into the S MFMA's accumulator
-#endif
-constexpr float ATT_THR = 8.0f;  // (LGM_AB_ATT 2) forward: the row reference m is raised only when a score exceeds it
-                                 // by more than this (log2 units): P <= 2^8, exact either way
+// The softmax's affine parts ride on the MFMAs: the register operand (Q in the forward and dQ kernels, K in dK/dV)
+// is pre-scaled by scale * log2(e) (rounded to the 16-bit type once), so S comes out in log2 units, and the S / dP
+// accumulators start at -m (-lse') and -delta of their rows, so exp2's argument and dS's (dP - delta) factor leave
+// the MFMA ready: no per-score fma or subtract (profiles/r04: D = 32 fwd / dQ / dK,dV measured in DESIGN.md §4).
+constexpr float ATT_THR = 8.0f;  // forward: the row reference m is raised only when a score exceeds it by more than
+                                 // this (log2 units): P <= 2^8, exact either way
 template <int DT, int N>
 __device__ __forceinline__ void prescale(typename Ty<DT>::V8 (&v)[N], float c) {  // v *= c, rounded to the type
 #pragma unroll
@@ -479,14 +479,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
     for (int s = 0; s < QS; s++) {
         const int qr = q0 + 16 * s + r16;
         load_yfrag<DT, D>(qf[s], q + base + (long long)qr * ld, qr < L, g);
-        if (LGM_AB_ATT >= 2) prescale<DT, D / 32>(qf[s].v, c);  // scores come out in log2 units
+        prescale<DT, D / 32>(qf[s].v, c);  // scores come out in log2 units
     }
     f32x4 oacc[QS][D / 16], lacc[QS];
     float m[QS];
 #pragma unroll
     for (int s = 0; s < QS; s++) {
         lacc[s] = zero4();
-        m[s] = LGM_AB_ATT >= 2 ? 0.f : -INFINITY;
+        m[s] = 0.f;
 #pragma unroll
         for (int dt = 0; dt < D / 16; dt++) oacc[s][dt] = zero4();
     }
@@ -534,8 +534,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
                 kf[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
 #pragma unroll
             for (int s = 0; s < QS; s++) {
-                // (LGM_AB_ATT 2: the accumulator starts at -m, so the MFMA leaves exp2's argument itself)
-                f32x4 a = LGM_AB_ATT >= 2 ? f32x4{-m[s], -m[s], -m[s], -m[s]} : zero4();
+                f32x4 a = {-m[s], -m[s], -m[s], -m[s]};  // the MFMA leaves exp2's argument itself
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) a = mfma32<DT>(kf[cc], qf[s].v[cc], a);
                 sacc[s][sub] = a;
@@ -552,7 +551,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
         }
         // ---- online softmax per query sub-tile; P as the B operand (key order of tr_frag)
         V8 pb[QS][2];
-#if LGM_AB_ATT >= 2
         // x = score - m (log2 units) straight from the MFMA. The reference m is raised (and O, l rescaled, x
         // shifted) only on the first tile or where some x exceeds ATT_THR: P = 2^x <= 2^ATT_THR, so no per-tile row
         // max and no per-score fma
@@ -586,34 +584,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
 #pragma unroll
             for (int t = 0; t < 2; t++) lacc[s] = mfma32<DT>(ones, pb[s][t], lacc[s]);
         }
-#else
-#pragma unroll
-        for (int s = 0; s < QS; s++) {
-            float mx = fmaxf(fmaxf(sacc[s][0][0], sacc[s][0][1]), fmaxf(sacc[s][0][2], sacc[s][0][3]));
-#pragma unroll
-            for (int sub = 1; sub < 4; sub++)
-                mx = fmaxf(fmaxf(mx, sacc[s][sub][0]), fmaxf(fmaxf(sacc[s][sub][1], sacc[s][sub][2]), sacc[s][sub][3]));
-            mx = xmax_groups(mx);
-            if (__ballot(mx > m[s])) {  // some row max grew: rescale (exactly, no threshold)
-                const float mn = fmaxf(m[s], mx);
-                const float alpha = __builtin_amdgcn_exp2f((m[s] - mn) * c);  // 0 on the first tile
-#pragma unroll
-                for (int dt = 0; dt < D / 16; dt++) oacc[s][dt] *= alpha;
-                lacc[s] *= alpha;
-                m[s] = mn;
-            }
-            const float nm = -m[s] * c;
-#pragma unroll
-            for (int t = 0; t < 2; t++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    pb[s][t][i] = (T)__builtin_amdgcn_exp2f(fmaf(sacc[s][2 * t][i], c, nm));
-                    pb[s][t][4 + i] = (T)__builtin_amdgcn_exp2f(fmaf(sacc[s][2 * t + 1][i], c, nm));
-                }
-#pragma unroll
-            for (int t = 0; t < 2; t++) lacc[s] = mfma32<DT>(ones, pb[s][t], lacc[s]);
-        }
-#endif
         // ---- O^T += V^T P
 #pragma unroll
         for (int t = 0; t < 2; t++)
@@ -641,7 +611,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
             for (int dt = 0; dt < D / 16; dt++)
 #pragma unroll
                 for (int i = 0; i < 4; i++) orow[16 * dt + 4 * g + i] = from_f<T>(oacc[s][dt][i] * inv);
-            if (g == 0) lse[(long long)bh * L + qr] = ((LGM_AB_ATT >= 2 ? m[s] : m[s] * c) + log2f(l)) * LN2;
+            if (g == 0) lse[(long long)bh * L + qr] = (m[s] + log2f(l)) * LN2;
         }
     }
 }
@@ -700,7 +670,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         const int kr = k0 + 16 * s + r16;
         load_yfrag<DT, D>(kf[s], k + base + (long long)kr * ld, kr < L, g);
         load_yfrag<DT, D>(vf[s], v + base + (long long)kr * ld, kr < L, g);
-        if (LGM_AB_ATT >= 2) prescale<DT, D / 32>(kf[s].v, c);  // S in log2 units
+        prescale<DT, D / 32>(kf[s].v, c);  // S in log2 units
     }
     f32x4 dka[KS][D / 16], dva[KS][D / 16];
 #pragma unroll
@@ -738,14 +708,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                 qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
                 orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
             }
-            // (LGM_AB_ATT: the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i)
-            f32x4 ainit = zero4(), dinit = zero4();
-            if (LGM_AB_ATT >= 1)
+            // (the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i)
+            f32x4 ainit, dinit;
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    if (LGM_AB_ATT >= 2) ainit[i] = -sl[cur][16 * sub + 4 * g + i];
-                    dinit[i] = -sd[cur][16 * sub + 4 * g + i];
-                }
+            for (int i = 0; i < 4; i++) {
+                ainit[i] = -sl[cur][16 * sub + 4 * g + i];
+                dinit[i] = -sd[cur][16 * sub + 4 * g + i];
+            }
 #pragma unroll
             for (int s = 0; s < KS; s++) {
                 f32x4 a = ainit, dp = dinit;
@@ -763,12 +732,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         for (int sub = 0; sub < 4; sub++)
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const int qi = 16 * sub + 4 * g + i;
-                const float l2 = sl[cur][qi], dl = sd[cur][qi];
 #pragma unroll
                 for (int s = 0; s < KS; s++) {
-                    const float p = __builtin_amdgcn_exp2f(LGM_AB_ATT >= 2 ? sacc[s][sub][i] : fmaf(sacc[s][sub][i], c, -l2));
-                    const float ds = p * (LGM_AB_ATT >= 1 ? dpa[s][sub][i] : dpa[s][sub][i] - dl);
+                    const float p = __builtin_amdgcn_exp2f(sacc[s][sub][i]);
+                    const float ds = p * dpa[s][sub][i];
                     pb[s][sub >> 1][4 * (sub & 1) + i] = (T)p;
                     db[s][sub >> 1][4 * (sub & 1) + i] = (T)ds;
                 }
@@ -835,7 +802,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         load_yfrag<DT, D>(of[s], dout + obase + (long long)qr * H * D, qv, g);
         l2[s] = qv ? lse[(long long)bh * L + qr] * LOG2E : INFINITY;
         dl[s] = qv ? delta[(long long)bh * L + qr] : 0.f;
-        if (LGM_AB_ATT >= 2) prescale<DT, D / 32>(qf[s].v, c);  // S in log2 units
+        prescale<DT, D / 32>(qf[s].v, c);  // S in log2 units
     }
     f32x4 dqa[QS][D / 16];
 #pragma unroll
@@ -865,9 +832,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
             }
 #pragma unroll
             for (int s = 0; s < QS; s++) {
-                // (LGM_AB_ATT: the accumulators start at -lse' / -delta of the lane's query)
-                f32x4 a = LGM_AB_ATT >= 2 ? f32x4{-l2[s], -l2[s], -l2[s], -l2[s]} : zero4();
-                f32x4 dp = LGM_AB_ATT >= 1 ? f32x4{-dl[s], -dl[s], -dl[s], -dl[s]} : zero4();
+                // (the accumulators start at -lse' / -delta of the lane's query)
+                f32x4 a = {-l2[s], -l2[s], -l2[s], -l2[s]};
+                f32x4 dp = {-dl[s], -dl[s], -dl[s], -dl[s]};
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
                     a = mfma32<DT>(kr[cc], qf[s].v[cc], a);    // S^T[key = 16 sub + 4g + i][q]
@@ -885,11 +852,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                 const bool kv = !TAIL || kb + 16 * sub + 4 * g + i < L;
 #pragma unroll
                 for (int s = 0; s < QS; s++) {
-                    const float p = kv ? __builtin_amdgcn_exp2f(LGM_AB_ATT >= 2 ? sacc[s][sub][i]
-                                                                                : fmaf(sacc[s][sub][i], c, -l2[s]))
-                                       : 0.f;
-                    db[s][sub >> 1][4 * (sub & 1) + i] =
-                        (T)(p * (LGM_AB_ATT >= 1 ? dpa[s][sub][i] : dpa[s][sub][i] - dl[s]));
+                    const float p = kv ? __builtin_amdgcn_exp2f(sacc[s][sub][i]) : 0.f;
+                    db[s][sub >> 1][4 * (sub & 1) + i] = (T)(p * dpa[s][sub][i]);
                 }
             }
 #pragma unroll

@@ -177,43 +177,21 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
             const size_t k = (size_t)bv * d.N + i;
             if (vis) {
                 const float4 rp = rec_p(o.x, o.y, o.A, o.B), rq = rec_q(o.C, o.opacity, o.tau, o.depth);
-                st_wt(gP + k, rp);  // pre-scaled compositing records (render_common.h)
-                st_wt(gQ + k, rq);
+                gP[k] = rp;  // pre-scaled compositing records (render_common.h)
+                gQ[k] = rq;
                 const bool side = !(d.options & LGM_RENDER_DETERMINISTIC) && rec_needle(rp.z, rp.w, rq.x);
-                st_wt(rects + k, make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16),
-                                            (unsigned)o.x1 | ((unsigned)o.y1 << 16) | (side ? 0x80000000u : 0u)));
+                rects[k] = make_uint2((unsigned)o.x0 | ((unsigned)o.y0 << 16),
+                                      (unsigned)o.x1 | ((unsigned)o.y1 << 16) | (side ? 0x80000000u : 0u));
                 if (side) {  // the record's fp64 conic accumulators (acc_side_offset)
                     double *sd = reinterpret_cast<double *>(accum + acc_side_offset(d.B, d.V, d.N)) + k * 3;
                     sd[0] = 0.0; sd[1] = 0.0; sd[2] = 0.0;
                 }
-                // the backward's per-view gradient accumulators start at zero (a repeated backward clears them with
-                // LGM_RENDER_BACKWARD_AGAIN); int64 fixed point in deterministic mode
-                if (LGM_AB_ZF) {
-                } else if (d.options & LGM_RENDER_DETERMINISTIC) {  // 8-B elements (int64)
-                    ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(accum) + k * (NACC_V / 2);
-#pragma unroll
-                    for (int q = 0; q < NACC_V / 2; q++) a2[q] = make_ulonglong2(0ull, 0ull);
-                } else {
-                    float2 *a2 = reinterpret_cast<float2 *>(accum + k * NACC_V);
-#pragma unroll
-                    for (int q = 0; q < NACC_V / 2; q++) a2[q] = make_float2(0.f, 0.f);
-                }
             } else {
-                st_wt(gP + k, make_float4(0.f, 0.f, 0.f, 0.f));
-                st_wt(gQ + k, make_float4(0.f, -INFINITY, -1.f, 0.f));
-                st_wt(rects + k, make_uint2(0u, 0u));
+                gP[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                gQ[k] = make_float4(0.f, -INFINITY, -1.f, 0.f);
+                rects[k] = make_uint2(0u, 0u);
             }
             if (radii_out) radii_out[k] = vis ? o.radius : 0;
-            if (!LGM_AB_ZF && bv % d.V == 0) {  // the scene's view-independent record (opacity, colour), once per scene
-                const size_t ks = (size_t)d.BV * d.N * NACC_V + ((size_t)b * d.N + i) * NACC_S;
-                if (d.options & LGM_RENDER_DETERMINISTIC) {  // 8-B elements (int64)
-                    ulonglong2 *a2 = reinterpret_cast<ulonglong2 *>(reinterpret_cast<unsigned long long *>(accum) + ks);
-                    a2[0] = make_ulonglong2(0ull, 0ull);
-                    a2[1] = make_ulonglong2(0ull, 0ull);
-                } else {
-                    *reinterpret_cast<float4 *>(accum + ks) = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-            }
         }
     }
     int nc = 0;
@@ -286,7 +264,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         if (pass == 1) {
             for (int k = 0; k < cnt; k++) {
                 const int t = trow + ta + k;
-                st_wt(pairs + dest(t, hbase[t] + atomicAdd(&fill[t], 1)), srec[owner].key);
+                pairs[dest(t, hbase[t] + atomicAdd(&fill[t], 1))] = srec[owner].key;
             }
             continue;
         }
@@ -313,7 +291,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
             for (int k = 0; k < cnt; k++) {
                 const int t = trow + ta + k;
                 const int pos = atomicAdd(&cur[t], 1);
-                if (MODE != COUNT) st_wt(pairs + dest(t, pos), srec[owner].key);
+                if (MODE != COUNT) pairs[dest(t, pos)] = srec[owner].key;
             }
         }
     }
@@ -339,7 +317,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                 for (int h = tid; h < H; h += BIN_THREADS) {
                     const unsigned e2 = sHit[h];
                     const int t = (int)(e2 >> 9);
-                    st_wt(pairs + dest(t, hbase[t] + sRank[h]), srec[e2 & 511u].key);
+                    pairs[dest(t, hbase[t] + sRank[h])] = srec[e2 & 511u].key;
                 }
             } else {
                 flat_tests(1);  // hit-list overflow: the wave's tests again, emitting with LDS fill ranks
@@ -354,6 +332,8 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         stamp[3] = ph_acc[2];
         stamp[4] = t_ph;
         stamp[5] = (unsigned long long)s_nhit;
+        stamp[6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID (SE / CU / SIMD / wave slot)
+        stamp[7] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
     }
     }  // batches
     if (tid == 0) {
@@ -599,24 +579,11 @@ __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const un
     const int shift = kbits > MSD_BITS ? kbits - MSD_BITS : 0;
     constexpr int BPT = MSD_B / RS_THREADS;
     // (hc and *s_flag were zeroed by sort_tile under its span barrier)
-#if LGM_AB_SORTH
-    // the histogram atomics return each entry's arrival rank in its bucket: kept (two u16 per register) as its slot
-    // offset, so the scatter needs no second round of atomics
-    unsigned offp[(RS_MAXR + 1) / 2];
-#pragma unroll
-    for (int r = 0; r < (RS_MAXR + 1) / 2; r++) offp[r] = 0u;
-#pragma unroll
-    for (int r = 0; r < RS_MAXR; r++) {
-        const int e = c0 + r * 64 + lane;
-        if (r < R && e < n) offp[r >> 1] |= atomicAdd(&hc[kr[r] >> shift], 1u) << (16 * (r & 1));
-    }
-#else
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         const int e = c0 + r * 64 + lane;
         if (r < R && e < n) atomicAdd(&hc[kr[r] >> shift], 1u);
     }
-#endif
     __syncthreads();
     // exclusive scan of the bucket counts (BPT consecutive buckets per thread), and the largest bucket
     unsigned loc[BPT], sum = 0u, mx = 0u;
@@ -643,21 +610,6 @@ __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const un
     // key and id side by side (the sk / si image read as one u64 array): one 8-B LDS write per entry here and one
     // 8-B read per bucket entry in the ranking, on the composite (key << 32 | id) order
     unsigned long long *skv = reinterpret_cast<unsigned long long *>(sk);
-#if LGM_AB_SORTH
-    // (hc[b] stays the START of bucket b; its end is hc[b + 1], or n for the last bucket)
-#pragma unroll
-    for (int r = 0; r < RS_MAXR; r++) {
-        const int e = c0 + r * 64 + lane;
-        if (r < R && e < n)
-            skv[hc[kr[r] >> shift] + ((offp[r >> 1] >> (16 * (r & 1))) & 0xffffu)] =
-                ((unsigned long long)kr[r] << 32) | ir[r];
-    }
-    __syncthreads();
-    for (int q = tid; q < n; q += RS_THREADS) {
-        const unsigned long long cq = skv[q];
-        const unsigned bq = (unsigned)(cq >> 32) >> shift;
-        const int lo = (int)hc[bq], hi = bq + 1 < (unsigned)MSD_B ? (int)hc[bq + 1] : n;
-#else
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         const int e = c0 + r * 64 + lane;
@@ -671,10 +623,9 @@ __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const un
         const unsigned long long cq = skv[q];
         const unsigned bq = (unsigned)(cq >> 32) >> shift;
         const int lo = bq ? (int)hc[bq - 1] : 0, hi = (int)hc[bq];
-#endif
         int rank = lo;
         for (int z = lo; z < hi; z++) rank += skv[z] < cq ? 1 : 0;
-        st_wt(ids_out + rank, (unsigned)cq);
+        ids_out[rank] = (unsigned)cq;
     }
     return true;
 }
@@ -851,7 +802,7 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         const int e = c0 + r * 64 + lane;
-        if (r < R && e < n) st_wt(ids + e, idr[r]);
+        if (r < R && e < n) ids[e] = idr[r];
     }
 }
 

@@ -8,8 +8,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <type_traits>
-
 #include "common.h"
 #include "lgm_render.h"
 
@@ -19,7 +17,7 @@ constexpr int BX = 16, BY = 16, TILE_PIX = BX * BY;  // 256 pixels per tile = 4 
 constexpr int NACC = 10;  // gradient partials per (view, Gaussian): mean2D(2) conic(3) opacity rgb(3) depth
 // Accumulator layout (elements: fp32, or int64 fixed point in deterministic mode): the view-dependent partials
 // (mean2D, conic, depth) per (view, Gaussian) in records of NACC_V, then the view-independent ones (opacity,
-// colour) per (scene, Gaussian) in records of NACC_S -- the views of a scene add into one record, so the binning
+// colour) per (scene, Gaussian) in records of NACC_S -- the views of a scene add into one record, so the forward
 // zeroes and k_preproc_bwd reads 24 + 16 / V bytes per (view, Gaussian) instead of 40.
 constexpr int NACC_V = 6, NACC_S = 4;
 __host__ __device__ __forceinline__ size_t acc_index(int q, size_t bvN_i, size_t bN_i, size_t BVN) {
@@ -47,46 +45,6 @@ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // the fp32 oracle's error vs fp64 at 512^2, profiles/r03/diag_float_spread); fp64 sums of the same fp32 partials are
 // order-independent to ~2^-50 of the partials (the deterministic mode's int64 sums are exact). Measured: all
 // accumulators fp64 +37 us per pool step, the needle side accumulators +24 us (profiles/r03/ab_acc_side).
-#ifndef LGM_AB_SORTH
-#define LGM_AB_SORTH 0  // (A/B in progress) 1: k_sort keeps the histogram atomics' ranks (no scatter atomics)
-#endif
-#ifndef LGM_AB_BWDQ
-#define LGM_AB_BWDQ 0  // (A/B in progress) 1: the one-wavefront-per-item backward (k_render_bwdq)
-#endif
-#ifndef LGM_AB_BCH
-#define LGM_AB_BCH 0  // (A/B in progress) 1: backward transmittance T (1 - alpha) as the forward's (1-op recurrence)
-#endif
-#ifndef LGM_AB_FCH
-#define LGM_AB_FCH 0  // (A/B in progress) 1: forward transmittance as an unconditional product (1-op recurrence)
-#endif
-#ifndef LGM_AB_ZF
-#define LGM_AB_ZF 0  // (A/B in progress) 1: k_render_fwd zeroes the gradient accumulators instead of k_bin
-#endif
-#ifndef LGM_AB_WT
-#define LGM_AB_WT 0  // (A/B in progress) 1: the kernels' hand-off outputs stored write-through (sc1)
-#endif
-// Stores of data the NEXT kernel reads (from any XCD): write-through (sc1 -- an agent-scope relaxed atomic store),
-// so the line leaves the XCD's L2 at once instead of being written back, dirty, at the kernel boundary (which
-// costs ~ dirty bytes / 6 TB/s on top of the ~1.7 us launch gap: MI355X_MICROARCH.md price list, "boundary").
-template <class T>
-__device__ __forceinline__ void st_wt(T *p, T v) {
-    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-B write-through stores");
-    if (LGM_AB_WT) {
-        using U = typename std::conditional<sizeof(T) == 4, unsigned, unsigned long long>::type;
-        __hip_atomic_store(reinterpret_cast<U *>(p), __builtin_bit_cast(U, v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        *p = v;
-    }
-}
-__device__ __forceinline__ void st_wt(float4 *p, float4 v) {
-    if (LGM_AB_WT) {
-        st_wt(reinterpret_cast<float2 *>(p), make_float2(v.x, v.y));
-        st_wt(reinterpret_cast<float2 *>(p) + 1, make_float2(v.z, v.w));
-    } else {
-        *p = v;
-    }
-}
 constexpr float ACC_NEEDLE = 300.0f;  // conic condition above which a record's conic partials are summed in fp64
 
 // Workspace layout. Pair storage `pairs` holds one u64 key (depth_bits << 32 | gaussian id) per (Gaussian, tile)

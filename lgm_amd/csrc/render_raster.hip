@@ -235,11 +235,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     init_sentinel(S);
     // Tr < 0 marks a saturated pixel (|Tr| its final transmittance): outside pixels start saturated
     float Tr = inside ? 1.0f : -1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
-#if LGM_AB_FCH
-    // T: the running product of (1 - alpha), never frozen (the recurrence is one multiply per entry); Tr: the
-    // transmittance upstream reports, frozen at termination. T < 1e-4 <=> terminated (T only decreases).
-    float T = inside ? 1.0f : 0.0f;
-#endif
     int last = 0;
     constexpr int FU = FWD_FU;
     unsigned c_iter = 0, c_list = 0;  // diagnostic work counters (Dims::counters)
@@ -258,11 +253,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     int ck_slot = -1, ck_written = 0;  // thread 0: slot reserved for the next boundary; checkpoints written
     for (int b0 = 0, c = 0; b0 < n; b0 += TILE_PIX, c++) {
         if (tid == 0) s_ck[c & 1] = ck_slot;  // reserved during chunk c - 1 (its atomic has long returned)
-#if LGM_AB_FCH
-        if (__syncthreads_count(!(T >= 0.0001f)) == TILE_PIX) break;  // also: every wave is done with the previous chunk
-#else
         if (__syncthreads_count(Tr < 0.f) == TILE_PIX) break;  // also: every wave is done with the previous chunk
-#endif
         c_list += min(TILE_PIX, n - b0);
         const int k = b0 + tid;
         StageBuf &B = S.buf[0];
@@ -287,13 +278,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 // and its reload's vmcnt(0) waited for the chunk's outstanding loads)
                 asm volatile("" : "+v"(ctid));
                 float *cp = ck + (size_t)sl * 5 * TILE_PIX + ctid;
-                cp[0] = LGM_AB_FCH ? Tr : fabsf(Tr);  // (plain stores: a write-through form spills here)
+                cp[0] = fabsf(Tr);
                 cp[TILE_PIX] = C0;
                 cp[2 * TILE_PIX] = C1;
                 cp[3 * TILE_PIX] = C2;
                 cp[4 * TILE_PIX] = D;
                 if (tid == 0) {
-                    st_wt(cklist + sl, make_int2(tile, c));
+                    cklist[sl] = make_int2(tile, c);
                     ck_written = c;
                 }
             }
@@ -307,11 +298,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         uint2 lraw[FU / 4];  // the next step's list words, read one step ahead (the list is fixed for the chunk)
         list_raw<FU>(S, w, 0, lraw);
         for (int kk = 0; kk < cnt; kk += FU) {
-#if LGM_AB_FCH
-            if (__ballot(T >= 0.0001f) == 0ull) break;
-#else
             if (__ballot(Tr > 0.f) == 0ull) break;
-#endif
             c_iter += min(FU, cnt - kk);
             int jj[FU];
             list_decode<FU>(lraw, jj);
@@ -343,23 +330,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             // so the FU evaluations above stay independent): upstream's test_T = T (1 - alpha) and T < 1e-4
             // termination, with the termination kept in Tr's sign -- a skipped entry (alpha 0) leaves test_T = T,
             // a saturated pixel (Tr < 0) has test_T <= 0, so one compare decides both
-#if LGM_AB_FCH
-#pragma unroll
-            for (int u = 0; u < FU; u++) {
-                const float alpha = al[u];
-                const float test_T = T * (1 - alpha);
-                const bool keep = test_T >= 0.0001f;
-                const float aw = keep ? alpha * T : 0.f;
-                C0 = fmaf(cc[u].x, aw, C0);
-                C1 = fmaf(cc[u].y, aw, C1);
-                C2 = fmaf(cc[u].z, aw, C2);
-                D = fmaf(cc[u].w, aw, D);
-                Tr = keep ? test_T : Tr;
-                T = test_T;
-                const bool acc = keep && alpha != 0.f;
-                last = acc ? b0 + jj[u] + 1 : last;
-            }
-#else
 #pragma unroll
             for (int u = 0; u < FU; u++) {
                 const float alpha = al[u];
@@ -374,24 +344,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 const bool acc = keep && alpha != 0.f;
                 last = acc ? b0 + jj[u] + 1 : last;
             }
-#endif
         }
     }
-    if (LGM_AB_ZF && zero_n16 > 0) {
+    if (zero_n16 > 0) {
         // this workgroup's slice of the backward's gradient accumulators (per-view and per-scene records, fp32 or
         // int64): zeroed here, at the end of the compositing, where the stores have the rest of the launch to drain,
-        // instead of in the binning's critical path
+        // instead of in the binning's critical path (pool / single scene -8 / -2 us, profiles/r04/ab_zf)
         const long long per = (zero_n16 + gridDim.x - 1) / gridDim.x, z0 = per * blockIdx.x;
         const long long z1 = min(zero_n16, z0 + per);
-        for (long long q = z0 + tid; q < z1; q += TILE_PIX) st_wt(zero_base + q, make_float4(0.f, 0.f, 0.f, 0.f));
+        for (long long q = z0 + tid; q < z1; q += TILE_PIX) zero_base[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (tid == 0) {
-        if (ck_slot >= 0) st_wt(cklist + ck_slot, make_int2(-1, 0));  // reserved for a boundary never reached
-        st_wt(nck + tile, ck_written);  // checkpoints c = 1 .. ck_written exist (a prefix: the counters only grow)
+        if (ck_slot >= 0) cklist[ck_slot] = make_int2(-1, 0);  // reserved for a boundary never reached
+        nck[tile] = ck_written;  // checkpoints c = 1 .. ck_written exist (a prefix: the counters only grow)
     }
     {  // the wave's largest last contributor (outside pixels: 0), for the backward's list bounds
         const int wl = wave_max_i32(last);
-        if (lane == 0) st_wt(wlast_out + 4 * (size_t)tile + w, wl);
+        if (lane == 0) wlast_out[4 * (size_t)tile + w] = wl;
     }
     if (d.counters) {
         // per-workgroup timeline (100 MHz s_memrealtime ticks): [8 + 8 tile] start, +1 end, +7 entries staged (low
@@ -411,11 +380,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     }
     float lsq_img = 0.f, lsq_a = 0.f;  // fused loss: this pixel's squared residuals
     if (inside) {
-        if (!LGM_AB_FCH) Tr = fabsf(Tr);  // (the sign only marked saturation)
+        Tr = fabsf(Tr);  // (the sign only marked saturation)
         const size_t P = (size_t)d.H * d.W;
         const size_t pid = (size_t)d.W * py + px;
-        st_wt(final_T + bv * P + pid, Tr);
-        st_wt(n_contrib + bv * P + pid, last);
+        final_T[bv * P + pid] = Tr;
+        n_contrib[bv * P + pid] = last;
         float *img = out_img + (size_t)bv * 3 * P;
         // explicit FMAs: the fused loss's backward recomputes these values bit for bit from cfin and final_T
         float c0 = fmaf(Tr, bg[0], C0), c1 = fmaf(Tr, bg[1], C1), c2 = fmaf(Tr, bg[2], C2);
@@ -426,12 +395,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             c1 = fminf(fmaxf(c1, 0.f), 1.f);
             c2 = fminf(fmaxf(c2, 0.f), 1.f);
         }
-        st_wt(img + pid, c0);
-        st_wt(img + P + pid, c1);
-        st_wt(img + 2 * P + pid, c2);
-        st_wt(out_depth + bv * P + pid, D);
-        st_wt(out_alpha + bv * P + pid, 1 - Tr);
-        st_wt(cfin + bv * P + pid, make_float4(C0, C1, C2, D));  // pre-background totals for the backward
+        img[pid] = c0;
+        img[P + pid] = c1;
+        img[2 * P + pid] = c2;
+        out_depth[bv * P + pid] = D;
+        out_alpha[bv * P + pid] = 1 - Tr;
+        cfin[bv * P + pid] = make_float4(C0, C1, C2, D);  // pre-background totals for the backward
         if (LOSS) {
             // core/models.py:145-148: gt composited over the background, squared residuals of image and alpha
             const float m = d.gt_mask[bv * P + pid];
@@ -459,7 +428,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 
 // Fused loss, final reduction over the per-tile (image, alpha) partials, fixed order, one launch: workgroup g sums
 // tiles [g * LR_TILES, +LR_TILES) (each thread LR_PER independent loads, then a fixed tree), writes its double2
-// partial, and the workgroup that arrives last (a counter in the workspace, zeroed by the forward's binning and
+// partial, and the workgroup that arrives last (a counter in the workspace, zeroed by the forward's memset and
 // reset by that workgroup) sums the partials in workgroup order and writes
 // out = (loss_mse, mse_image, mse_alpha, psnr) as core/models.py:148 (F.mse_loss twice) and :167 (psnr).
 // (Was one workgroup looping over every tile: 38.8 us at cfg5's 26,624 tiles, now a few us.)
@@ -1008,11 +977,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                     const float inv = __builtin_amdgcn_rcpf(om);  // 1 / (1 - alpha), 1 ulp
                     Erem = fmaf(-aT, cdp, Erem);
                     const float dL_dalpha = fmaf(Tr, cdp, -Erem * inv);
-#if LGM_AB_BCH
-                    Tr = Tr * om;  // (the forward's recurrence: one dependent multiply per entry)
-#else
                     Tr = Tr - aT;
-#endif
                     myWU[(4 * h + u) * WU_LD + lane] = Gw[u] * dL_dalpha;  // w
                     myWU[(MB + 4 * h + u) * WU_LD + lane] = aT;            // u (dchannel_dcolor)
                 }
@@ -1157,364 +1122,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     }
 }
 
-// k_render_bwdq: the compositing backward with ONE WAVEFRONT per work item: item = (tile, quadrant, chunk), block 64.
-// Grid: 4 (B*V*T) head items (chunk 0 of every quadrant, a tile's four quadrants adjacent in the XCD order), padding
-// to a multiple of 32, then 4 per checkpoint slot (XCD group g = blockIdx % 8 takes region g's slots, used slots first;
-// unused ones exit at once). Same arithmetic as the per-tile form (prefix state, pixel-moment MFMAs, one flush per
-// (item, entry)), without any workgroup barrier: the wave stages its own 64-entry chunks (LDS DMA, ordered by its own
-// vmcnt), tests them against its quadrant, walks its list, converts its moments to partials lane-per-entry and flushes
-// them. A quadrant whose pixels are all done (positions >= its wlast) costs nothing, and a light quadrant's slot frees
-// as soon as it is done instead of waiting at the tile's barriers for the heaviest.
-// LDS per item: staging 3 x 65 x 16 B, list 72 x 2 B, moments NV x 65 x 4 B, w/u image 16 x 68 x 4 B (~9.9 KB: 16
-// items per CU, as the <= 128 VGPRs of 4 waves per SIMD).
-template <bool DEPTH, bool LOSS, bool DET>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 : 4))) void k_render_bwdq(
-    Dims d, long long slot_stride, const int *__restrict__ tile_start,
-    const int *__restrict__ tile_count, const unsigned long long *__restrict__ pairs, const float4 *__restrict__ gP,
-    const float4 *__restrict__ gQ, const float *__restrict__ gauss, const float *__restrict__ bg,
-    const float *__restrict__ final_T, const int *__restrict__ n_contrib, const int *__restrict__ wlast_fwd,
-    const float4 *__restrict__ cfin, const float *__restrict__ ck, const int2 *__restrict__ cklist,
-    const int *__restrict__ nck,
-    const unsigned *__restrict__ ckctr, int ck_region, const float *__restrict__ d_img,
-    const float *__restrict__ d_depth, const float *__restrict__ d_alpha, const unsigned char *__restrict__ cmask,
-    float *__restrict__ accum, const unsigned *__restrict__ det_max, unsigned *__restrict__ det_sat,
-    long long item_stamps) {
-    constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
-    constexpr int CH = 64, LS = CH + 1;          // entries per staged chunk; moment row stride (column CH: padding)
-    constexpr int NC = DEPTH ? 4 : 3;            // dL/dpixel channels in the moments
-    __shared__ StageBufT<CH> S;                  // rows 0..63, row 64 the sentinel; R.w holds the entry's id
-    __shared__ __attribute__((aligned(8))) unsigned short sList[CH + MB];  // read as 8-B words
-    // moment slots [NV rows][LS]: rows 0..5 the geometric moments of w, 6..6+NC-1 the dL/dpixel sums of u; after the
-    // conversion the entry's gradient partials in place
-    __shared__ __attribute__((aligned(16))) float sAcc[NV * LS];
-    __shared__ __attribute__((aligned(16))) float sWU[16 * WU_LD];  // w/u image (read as float4: 16-B aligned)
-
-    // ---- work item: (tile, quadrant qd, chunk c, checkpoint slot)
-    const int M = d.BV * d.T, Mp4 = 4 * round8(M);
-    const int bid = (int)blockIdx.x;
-    int tile, qd, c = 0, slot = -1;
-    if (bid < 4 * M) {
-        const int h = xcd_item(bid, 4 * M);
-        tile = h >> 2;
-        qd = h & 3;
-    } else {
-        if (bid < Mp4) return;  // padding: the checkpoint items start at a multiple of 32 (XCD g = bid % 8 = e % 8)
-        const int e = bid - Mp4, g = e & 7, i = e >> 3, l = i >> 2;
-        qd = i & 3;
-        if (l >= (int)ckctr[g]) return;  // an unused slot of region g (wave-uniform)
-        slot = l * 8 + g;
-        const int2 ce = cklist[slot];
-        if (ce.x < 0) return;  // reserved, never written
-        tile = ce.x;
-        c = ce.y;
-    }
-    const int lane = threadIdx.x;
-    const int4 wl4 = reinterpret_cast<const int4 *>(wlast_fwd)[tile];
-    const int wlast = qd == 0 ? wl4.x : qd == 1 ? wl4.y : qd == 2 ? wl4.z : wl4.w;  // this quadrant's list bound
-    const int s0 = c * TILE_PIX;
-    if (s0 >= wlast) return;  // every pixel of the quadrant was done before this chunk
-    const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
-    const int qx0 = (t % d.gx) * BX + ((qd & 1) << 3), qy0 = (t / d.gx) * BY + ((qd >> 1) << 3);
-    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);  // (tile_pixel of tid = 64 qd + lane)
-    const bool inside = px < d.W && py < d.H;
-    const float pfx = (float)px, pfy = (float)py;
-    long long base;
-    int n;
-    tile_range(tile, slot_stride, tile_start, tile_count, base, n);
-    const int nlist = min(n, wlast);
-    const int s1 = (c + 1 <= nck[tile]) ? min(nlist, s0 + TILE_PIX) : nlist;
-    if (s0 >= s1) return;
-    const unsigned *ids = reinterpret_cast<const unsigned *>(pairs + base);
-    const size_t gbase = (size_t)bv * d.N;
-    // the first chunk's ids and LDS DMA go out before the per-pixel state loads (their dependent round trips overlap)
-    unsigned id_cur = s0 + lane < s1 ? ids[s0 + lane] : 0u;
-    if (s0 + lane < s1) stage_dma(S, 0, id_cur, gbase, b, d.N, gP, gQ, gauss);
-    unsigned id_next = s0 + CH + lane < s1 ? ids[s0 + CH + lane] : 0u;
-    const size_t P = (size_t)d.H * d.W;
-    const size_t pid = inside ? (size_t)d.W * py + px : 0;
-    const float T_final = inside ? final_T[bv * P + pid] : 0.f;
-    const int last = inside ? n_contrib[bv * P + pid] : 0;
-    float ckT = 1.0f, ck1 = 0.f, ck2 = 0.f, ck3 = 0.f, ck4 = 0.f;
-    if (slot >= 0) {
-        const float *cp = ck + (size_t)slot * 5 * TILE_PIX + 64 * qd + lane;
-        ckT = cp[0];
-        ck1 = cp[TILE_PIX];
-        ck2 = cp[2 * TILE_PIX];
-        ck3 = cp[3 * TILE_PIX];
-        if (DEPTH) ck4 = cp[4 * TILE_PIX];
-    }
-    PixelSeed sd;
-    pixel_seed<DEPTH, LOSS>(d, inside, bv, P, pid, T_final, bg, cfin, d_img, d_depth, d_alpha, cmask, sd);
-    const float dp0 = sd.dp0, dp1 = sd.dp1, dp2 = sd.dp2, dpd = sd.dpd, dpa = sd.dpa;
-    const float4 cf = sd.cf;
-    float Tr = 1.0f, Dup = 0.f;  // per-pixel state entering the chunk: the forward's checkpoint (or the list head)
-    if (slot >= 0) {
-        Tr = ckT;
-        Dup = fmaf(ck1, dp0, fmaf(ck2, dp1, ck3 * dp2));
-        if (DEPTH) Dup = fmaf(ck4, dpd, Dup);
-    }
-    if (lane == 0) {  // the sentinel row (alpha 0)
-        S.P[CH] = make_float4(0.f, 0.f, 0.f, 0.f);
-        S.Q[CH] = make_float4(0.f, -INFINITY, 0.f, 0.f);
-        S.R[CH] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    const unsigned long long t_item = d.counters ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    const float bg_dot = bg[0] * dp0 + bg[1] * dp1 + bg[2] * dp2;
-    float cdpf = fmaf(cf.x, dp0, fmaf(cf.y, dp1, cf.z * dp2));
-    if (DEPTH) cdpf = fmaf(cf.w, dpd, cdpf);
-    const float DK = cdpf - (dpa - bg_dot) * T_final;  // Dfin - K
-    float Erem = DK - Dup;  // Dfin - K - D_i, kept directly (one subtraction less per entry)
-    const float ddelx_dx = 0.5f * d.W, ddely_dy = 0.5f * d.H;
-    const int det_s = DET ? det_seed_shift(det_max) : 0;
-    // MFMA operands: A (features) lane (ql, qk) holds feature row ql at the wave pixels 32 t2 + 8 qk + j, j = 0..7.
-    // Rows 0..5: the geometric features (exact in bf16); 6, 7: zero; 8 + 2 ch, 9 + 2 ch: dL/dpixel of channel ch
-    // (colour 0..2, depth) as bf16 hi and lo parts -- so the hi and lo sums of a channel land in the same lane's
-    // results (rows 4 qk .. 4 qk + 3) and are added there, and each lane keeps at most 4 results:
-    //   w columns (ql < 8): qk 0 -> moment rows 0..3, qk 1 -> rows 4, 5;  u columns (ql >= 8): qk 2 -> channels 0, 1,
-    //   qk 3 -> channel 2 [and depth].
-    const int ql = lane & 15, qk = lane >> 4;
-    const float cxT = (float)(qx0 - ((qd & 1) << 3)) + 7.5f, cyT = (float)(qy0 - ((qd >> 1) << 3)) + 7.5f;
-    float *myWU = sWU;
-    myWU[lane] = dp0;
-    myWU[64 + lane] = dp1;
-    myWU[128 + lane] = dp2;
-    myWU[192 + lane] = dpd;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    bf16x8 Ah[2];
-    {
-        const float fx0 = (float)((qd & 1) << 3) - 7.5f, fy0 = (float)((qd >> 1) << 3) - 7.5f;
-        const bool isdp = ql >= 8 && (DEPTH || ql < 14), islo = (ql & 1) != 0;
-        const int qch = isdp ? (ql - 8) >> 1 : 0;  // the dL/dpixel channel of rows 8..15
-#pragma unroll
-        for (int t2 = 0; t2 < 2; t2++) {
-            const float fy = fy0 + (float)(4 * t2 + qk);
-            const float ca = ql == 0 ? 1.f : ql == 1 ? fx0 : ql == 2 ? fy : ql == 3 ? fx0 * fx0
-                           : ql == 4 ? fx0 * fy : ql == 5 ? fy * fy : 0.f;
-            const float cb = ql == 1 ? 1.f : ql == 3 ? 2.f * fx0 : ql == 4 ? fy : 0.f;
-            const float cc2 = ql == 3 ? 1.f : 0.f;
-            const float4 *src = reinterpret_cast<const float4 *>(myWU + qch * 64 + 32 * t2 + 8 * qk);
-            const float4 d0 = src[0], d1 = src[1];
-            const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const float geo = fmaf(fmaf(cc2, (float)j, cb), (float)j, ca);
-                const __bf16 dh = (__bf16)dv[j];
-                const float dlo = dv[j] - (float)dh;
-                Ah[t2][j] = ql <= 5 ? (__bf16)geo : !isdp ? (__bf16)0.f : islo ? (__bf16)dlo : dh;
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // the moment rows this lane keeps (-1: none), and whether its result pairs are hi + lo sums (u columns)
-    int mrow[4];
-    const bool ucol = ql >= MB;
-#pragma unroll
-    for (int rr = 0; rr < 4; rr++) mrow[rr] = -1;
-    if (!ucol && qk == 0) { mrow[0] = 0; mrow[1] = LS; mrow[2] = 2 * LS; mrow[3] = 3 * LS; }
-    if (!ucol && qk == 1) { mrow[0] = 4 * LS; mrow[1] = 5 * LS; }
-    if (ucol && qk == 2) { mrow[0] = 6 * LS; mrow[1] = 7 * LS; }
-    if (ucol && qk == 3) { mrow[0] = 8 * LS; if (DEPTH) mrow[1] = 9 * LS; }
-    int myj = 0;  // the chunk row of this lane's batch column (ql & 7)
-    // B operand of the current batch: lane (ql, qk) takes column ql at pixels 32 t + 8 qk + j (two 16-B reads per t)
-    auto read_batch = [&](float (&xs)[2][8]) {
-#pragma unroll
-        for (int t2 = 0; t2 < 2; t2++) {
-            const float4 *src = reinterpret_cast<const float4 *>(myWU + ql * WU_LD + 32 * t2 + 8 * qk);
-            const float4 x0 = src[0], x1 = src[1];
-            xs[t2][0] = x0.x; xs[t2][1] = x0.y; xs[t2][2] = x0.z; xs[t2][3] = x0.w;
-            xs[t2][4] = x1.x; xs[t2][5] = x1.y; xs[t2][6] = x1.z; xs[t2][7] = x1.w;
-        }
-    };
-    // split hi + lo (round-to-nearest hi part: <= 2^-17 |x| per product, unbiased), the moment MFMAs, and the lane's
-    // (at most 4) kept results into the moment slots
-    auto mfma_batch = [&](const float (&xs)[2][8], int col) {
-        f32x4 a2[2];
-#pragma unroll
-        for (int t2 = 0; t2 < 2; t2++) {
-            bf16x8 bh, bl;
-#pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-                const bf16x2v hp = __builtin_convertvector((f32x2v){xs[t2][j], xs[t2][j + 1]}, bf16x2v);
-                const unsigned hb = __builtin_bit_cast(unsigned, hp);
-                const float h0 = __builtin_bit_cast(float, hb << 16), h1 = __builtin_bit_cast(float, hb & 0xffff0000u);
-                const bf16x2v lp = __builtin_convertvector((f32x2v){xs[t2][j] - h0, xs[t2][j + 1] - h1}, bf16x2v);
-                bh[j] = hp[0];
-                bh[j + 1] = hp[1];
-                bl[j] = lp[0];
-                bl[j + 1] = lp[1];
-            }
-            f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
-            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bh, cacc, 0, 0, 0);
-            cacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[t2], bl, cacc, 0, 0, 0);
-            a2[t2] = cacc;
-        }
-        const f32x4 acc = a2[0] + a2[1];
-        // u columns: rows (4 qk, 4 qk + 1) and (4 qk + 2, 4 qk + 3) are a channel's hi and lo sums
-        const float r0 = ucol ? acc[0] + acc[1] : acc[0], r1 = ucol ? acc[2] + acc[3] : acc[1];
-        if (mrow[0] >= 0) sAcc[mrow[0] + col] = r0;
-        if (mrow[1] >= 0) sAcc[mrow[1] + col] = r1;
-        if (mrow[2] >= 0) sAcc[mrow[2] + col] = acc[2];
-        if (mrow[3] >= 0) sAcc[mrow[3] + col] = acc[3];
-    };
-
-    const float qfx = (float)qx0, qfy = (float)qy0;
-    for (int b0 = s0; b0 < s1; b0 += CH) {
-        vm_wait_all();  // this chunk's rows (and ids, and the previous chunk's gradient atomics) have landed
-        reinterpret_cast<unsigned *>(&S.R[lane])[3] = id_cur;  // for the flush (the DMA leaves R.w alone)
-        // one row per lane: the entry against this quadrant (positions < wlast only); the ballot is the list
-        bool hit = false;
-        if (b0 + lane < s1) {
-            const float4 p = S.P[lane], q = S.Q[lane];
-            hit = rec_hits_rect(p, q, qfx, qfx + 7.0f, qfy, qfy + 7.0f);
-        }
-        const unsigned long long hitm = __ballot(hit);
-        if (hit) sList[__popcll(hitm & lanemask_lt(lane))] = (unsigned short)lane;
-        const int cnt = __popcll(hitm);
-        if (lane < MB) sList[cnt + lane] = (unsigned short)CH;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        const int lastrel = last - b0;  // this pixel's last contributor, relative to the chunk
-        uint2 lraw[2];  // the next step's list words, read one step ahead
-        lraw[0] = *reinterpret_cast<const uint2 *>(&sList[0]);
-        lraw[1] = *reinterpret_cast<const uint2 *>(&sList[4]);
-        auto eval_batch = [&](int kk) {
-            int jj8[MB];
-            list_decode<MB>(lraw, jj8);
-            myj = sList[kk + (lane & (MB - 1))];  // the entry of this lane's batch column
-            lraw[0] = *reinterpret_cast<const uint2 *>(&sList[kk + MB]);  // in bounds: the list holds CH + MB words
-            lraw[1] = *reinterpret_cast<const uint2 *>(&sList[kk + MB + 4]);
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                float al[4], Gw[4];
-                float4 cc[4], Pv[4], Qv[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {  // the LDS reads first, one wait (see k_render_fwd)
-                    const int j = jj8[4 * h + u];
-                    Pv[u] = S.P[j];
-                    Qv[u] = S.Q[j];
-                    const float4 Rj = S.R[j];
-                    cc[u] = make_float4(Rj.x, Rj.y, Rj.z, 0.f);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const bool before_last = jj8[4 * h + u] < lastrel;  // position b0 + jj < last
-                    const float4 Pj = Pv[u], Q = Qv[u];
-                    cc[u].w = Q.w;
-                    const float dx = Pj.x - pfx, dy = Pj.y - pfy;
-                    const float lp = fmaf(Q.x * dy, dy, fmaf(fmaf(Pj.w, dy, Pj.z * dx), dx, Q.y));  // as k_render_fwd
-                    const float e = __builtin_amdgcn_exp2f(lp);  // opacity G
-                    const bool ok = before_last && lp <= Q.y && e >= 1.0f / 255.0f;
-                    Gw[u] = ok ? e : 0.f;  // dL/dG = opacity dL/dalpha (0: the entry adds nothing here)
-                    al[u] = alpha_cap(Gw[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {  // the prefix recurrences in list order
-                    const float alpha = al[u];
-                    const float4 cu = cc[u];
-                    float cdp = fmaf(cu.x, dp0, fmaf(cu.y, dp1, cu.z * dp2));
-                    if (DEPTH) cdp = fmaf(cu.w, dpd, cdp);
-                    const float aT = alpha * Tr;
-                    const float inv = __builtin_amdgcn_rcpf(1.f - alpha);  // 1 / (1 - alpha), 1 ulp
-                    Erem = fmaf(-aT, cdp, Erem);
-                    const float dL_dalpha = fmaf(Tr, cdp, -Erem * inv);
-                    Tr = Tr - aT;
-                    myWU[(4 * h + u) * WU_LD + lane] = Gw[u] * dL_dalpha;  // w
-                    myWU[(MB + 4 * h + u) * WU_LD + lane] = aT;            // u (dchannel_dcolor)
-                }
-            }
-        };
-        // software-pipelined: batch k's B operand is read from the WU image BEFORE batch k + 1 overwrites it (a
-        // wave's LDS operations complete in issue order), so its LDS round trip and MFMAs overlap k + 1's evaluation
-        if (cnt > 0) {
-            eval_batch(0);
-            for (int kk = 0; kk < cnt; kk += MB) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                float xs[2][8];
-                read_batch(xs);
-                const int col = myj;
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // (the reads issue before the next writes)
-                if (kk + MB < cnt) eval_batch(kk + MB);
-                mfma_batch(xs, col);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        }
-        // moments -> gradient partials, lane j = entry j of the chunk (listed entries only), in place
-        unsigned long long ndlm = 0ull;  // needle-like listed entries: their conic partials go to the fp64 side block
-        if (hit) {
-            const int j = lane;
-            const float4 Pj = S.P[j];
-            const float4 Qj = S.Q[j];
-            float cA, cB, cC, op;  // the upstream conic and opacity
-            rec_conic(Pj, Qj, cA, cB, cC, op);
-            const float xg = Pj.x - cxT, yg = Pj.y - cyT;
-            float qm[NACC];
-#pragma unroll
-            for (int qq = 0; qq < NV; qq++) qm[qq] = sAcc[qq * LS + j];
-            const float Sx = fmaf(xg, qm[0], -qm[1]), Sy = fmaf(yg, qm[0], -qm[2]);
-            const float Sxx = fmaf(xg, fmaf(xg, qm[0], -2.f * qm[1]), qm[3]);
-            const float Sxy = fmaf(xg, fmaf(yg, qm[0], -qm[2]), fmaf(-yg, qm[1], qm[4]));
-            const float Syy = fmaf(yg, fmaf(yg, qm[0], -2.f * qm[2]), qm[5]);
-            float part[NACC];
-            part[0] = -ddelx_dx * (cA * Sx + cB * Sy);
-            part[1] = -ddely_dy * (cC * Sy + cB * Sx);
-            part[2] = -0.5f * Sxx;
-            part[3] = -0.5f * Sxy;
-            part[4] = -0.5f * Syy;
-            part[5] = op > 0.f ? qm[0] / op : 0.f;
-#pragma unroll
-            for (int qq = 6; qq < NV; qq++) part[qq] = qm[qq];
-            if (DET) {  // fixed-point units: the call's seed scale and the record's normalisers (exact powers of two)
-                const DetNorm nm = det_norm(Pj.z, Pj.w, Qj.x, d.W, d.H);
-#pragma unroll
-                for (int qq = 0; qq < NV; qq++) part[qq] = ldexpf(part[qq], det_s + (qq < 5 ? nm.k[qq] : 0));
-            }
-            if (!DET) ndlm = rec_needle(Pj.z, Pj.w, Qj.x) ? 1ull : 0ull;
-#pragma unroll
-            for (int qq = 0; qq < NV; qq++) sAcc[qq * LS + j] = part[qq];
-        }
-        ndlm = __ballot(ndlm != 0ull);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        // the next chunk's rows stream in during the flush (its P / Q / R.xyz overwrite this chunk's; R.w keeps the ids)
-        if (b0 + CH + lane < s1) stage_dma(S, 0, id_next, gbase, b, d.N, gP, gQ, gauss);
-        id_cur = id_next;
-        id_next = b0 + 2 * CH + lane < s1 ? ids[b0 + 2 * CH + lane] : 0u;
-        // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous records
-        int ft = lane;
-        asm volatile("" : "+v"(ft));  // (indices recomputed per chunk: hoisted, their 64-bit offsets spilled)
-        const size_t so = acc_side_offset(d.B, d.V, d.N) / 2;
-#pragma unroll
-        for (int it = 0; it < (CH * NACC + 63) / 64; it++) {
-            const int f = it * 64 + ft;
-            const int j = f / NACC, q = f - j * NACC;
-            if (q < NV && j < CH && ((hitm >> j) & 1ull)) {
-                const float a = sAcc[q * LS + j];
-                if (a != 0.f) {
-                    const unsigned gid = reinterpret_cast<const unsigned *>(&S.R[j])[3];
-                    if (DET) {  // integer adds commute: order-independent sums (a is already in fixed-point units)
-                        // (|a| <= ~2^51 per flush by design; beyond 2^62 counted: k_preproc_bwd poisons the call)
-                        if (!(fabsf(a) <= 0x1p62f)) atomicAdd(det_sat, 1u);
-                        atomicAdd(reinterpret_cast<unsigned long long *>(accum) +
-                                      acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N),
-                                  (unsigned long long)__float2ll_rn(fminf(fmaxf(a, -9.0e18f), 9.0e18f)));
-                    } else if (q >= 2 && q <= 4 && ((ndlm >> j) & 1ull)) {  // a needle's conic partial: fp64
-                        atomicAdd(reinterpret_cast<double *>(accum) + so + (gbase + gid) * 3 + (q - 2), (double)a);
-                    } else {
-                        atomicAdd(accum + acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N), a);
-                    }
-                }
-            }
-        }
-    }
-    // (no LDS DMA is in flight here: a chunk's DMA is issued only when another iteration, which waits for it, follows)
-    if (d.counters && lane == 0) {  // work-item timeline (lgm_diag.render_counters): start, end, (length | chunk | tile)
-        unsigned long long *o = d.counters + item_stamps + 4 * (size_t)blockIdx.x;
-        o[0] = t_item;
-        o[1] = __builtin_amdgcn_s_memrealtime();
-        o[2] = (unsigned long long)(s1 - s0) | ((unsigned long long)c << 20) | ((unsigned long long)tile << 40);
-        o[3] = (unsigned long long)qd;
-    }
-}
-
 // The preprocess backward's recomputation of the forward's projection (make_proj / cov2d / the homogeneous
 // divide): FP contraction on and 1-ulp v_rcp_f32 reciprocals. The forward keeps the oracle's bit-exact operation
 // order because its integer outputs (radii, tile rects, sort keys) depend on it; here the values only feed
@@ -1613,7 +1220,7 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
                 acc[2 * q] = (float)ldexp((double)a.x, -(det_s + nm.k[2 * q]));
                 acc[2 * q + 1] = (float)ldexp((double)a.y, -(det_s + nm.k[2 * q + 1]));
             }
-        } else {  // (zeroed by the forward's binning; see LGM_RENDER_BACKWARD_AGAIN)
+        } else {  // (zeroed by the forward's epilogue; see LGM_RENDER_BACKWARD_AGAIN)
 #pragma unroll
             for (int q = 0; q < NACC_V / 2; q++) {
                 acc[2 * q] = acc_e[q].x;
@@ -1770,7 +1377,7 @@ int launch_loss_reduce(const Dims &d, char *ws, const Layout &L, hipStream_t st)
 int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_view, const float *cam_view_proj,
                       const float *bg, const float *d_image, const float *d_depth, const float *d_alpha,
                       float *d_gaussians, float *d_means2D, char *ws, const Layout &L, hipStream_t st) {
-    // the per-view accumulators were zeroed by the forward's binning; a repeated backward of the same forward
+    // the accumulators were zeroed by the forward (k_render_fwd's epilogue); a repeated backward of the same forward
     // clears what the previous one left
     if ((d.options & LGM_RENDER_BACKWARD_AGAIN) &&
         hipMemsetAsync(ws + L.accum, 0, (d.options & LGM_RENDER_DETERMINISTIC)
@@ -1794,25 +1401,15 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
                                              d_image, d_depth, d_alpha, (const unsigned char *)(ws + L.cmask),
                                              det_max)));
     }
-#if LGM_AB_BWDQ
-    auto pick = [&](auto depth_tag) {
-        constexpr bool DP = decltype(depth_tag)::value;
-        return loss ? (det ? k_render_bwdq<DP, true, true> : k_render_bwdq<DP, true, false>)
-                    : (det ? k_render_bwdq<DP, false, true> : k_render_bwdq<DP, false, false>);
-    };
-    constexpr int QW = 4, BT = 64;  // one wavefront per (tile quadrant, chunk)
-#else
     auto pick = [&](auto depth_tag) {
         constexpr bool DP = decltype(depth_tag)::value;
         return loss ? (det ? k_render_bwd<DP, true, true> : k_render_bwd<DP, true, false>)
                     : (det ? k_render_bwd<DP, false, true> : k_render_bwd<DP, false, false>);
     };
-    constexpr int QW = 1, BT = 256;
-#endif
     auto bwd = d_depth ? pick(std::true_type{}) : pick(std::false_type{});
     // work items: chunk 0 of every tile, then one per checkpoint slot (unused slots exit at once)
     const int M = d.BV * d.T, Mp = round8(M);
-    LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(QW * (Mp + L.ck_slots)), BT, 0, st>>>(
+    LGM_LAUNCH("k_render_bwd", st, (bwd<<<(unsigned)(Mp + L.ck_slots), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),
                                        (const float4 *)(ws + L.gP), (const float4 *)(ws + L.gQ), gaussians, bg,

@@ -24,7 +24,7 @@ d_img, _, d_alpha, bg = synthetic_upstream_grads(B, V, 256, 256, seed=1001 if B 
 d_img, d_alpha, bg = d_img.to(dev), d_alpha.to(dev), bg.to(dev)
 M = B * V * 256
 NB = B * V * ((N + 511) // 512)  # binning records reserved (k_bin uses B * ceil(V / 3) * ceil(N / 512))
-NI = 12 * M + 256  # backward work-item capacity (the one-wave backward: 4 items per tile and per checkpoint slot)
+NI = 3 * M + 16  # backward work items: one per tile (rounded up to 8) and one per checkpoint slot (include/lgm_render.h)
 cnt = torch.zeros(8 + 8 * M + 8 * NB + 4 * NI, dtype=torch.int64, device=dev)
 
 

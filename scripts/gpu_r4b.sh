@@ -32,4 +32,7 @@ step tl_bwdq
 LGM_AMD_LIB=$V/lib_bwdq.so timeout -k 10 150 python scripts/diag_timeline.py 1 > gpurun_out/tl1_bwdq.log 2>&1 || exit $?
 mv gpurun_out/timeline_B1.npz gpurun_out/timeline_B1_bwdq.npz
 grep -v amdgpu.ids gpurun_out/tl1_bwdq.log
+step tl_hw  # the in-tree library (default build, with the forward's hardware-placement stamps)
+timeout -k 10 150 python scripts/diag_timeline.py 1 > gpurun_out/tl1_hw.log 2>&1 || exit $?
+mv gpurun_out/timeline_B1.npz gpurun_out/timeline_B1_hw.npz
 exit $rc

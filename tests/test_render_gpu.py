@@ -124,7 +124,7 @@ def test_forward_deterministic(cuda):
 
 
 def test_repeated_backward_retain_graph(cuda):
-    """A second backward of one forward (retain_graph) gives the first one's gradient: the forward's binning zeroes
+    """A second backward of one forward (retain_graph) gives the first one's gradient: the forward zeroes
     the accumulators, and the repeat clears what the first backward left (LGM_RENDER_BACKWARD_AGAIN)."""
     g, cv, cvp = scene(N=3000, V=2, seed=5)
     gd = g.to(cuda).requires_grad_(True)

@@ -83,6 +83,12 @@ struct StageT {                                   // PAD: list padding = entries
 constexpr int FWD_FU = 4;
 using StageFwd = StageT<1, FWD_FU>;
 constexpr int BWD_CHUNK = 64;
+#ifndef LGM_AB_NB
+#define LGM_AB_NB 0  // (A/B in progress) 1: per-wave slot zeroing, no barrier between the quadrant tests and the entries
+#endif
+#ifndef LGM_AB_CONV
+#define LGM_AB_CONV 0  // (A/B in progress) 1: the moments -> partials conversion split over three waves
+#endif
 // backward lists are padded to MB with the sentinel: every list position is one MFMA batch column (k_render_bwd)
 using StageBwd = StageT<2, MB, BWD_CHUNK>;
 
@@ -694,8 +700,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // moment rows: 0..5 geometric (w columns), then dL/dpixel-hi and dL/dpixel-lo sums of the NC colour [+ depth]
     // channels (u columns); row NROW is the junk row
     constexpr int NC = DEPTH ? 4 : 3, NROW = 6 + 2 * NC;
-    __shared__ __attribute__((aligned(16))) float sAccW[4][LS * (NROW + 1)];
+    constexpr int SLOT = LGM_AB_NB ? (LS * (NROW + 1) + 3) & ~3 : LS * (NROW + 1);  // (NB: 16-B aligned slots)
+    __shared__ __attribute__((aligned(16))) float sAccW[4][SLOT];
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
+    static_assert(!LGM_AB_CONV || (NV + 3) * LS <= 16 * WU_LD, "the partial rows fit wave 0's WU image");
     __shared__ int s_ndl;  // the chunk holds a needle-like record (its conic partials go to the fp64 side block)
 
     // ---- work item: (tile, chunk c, checkpoint slot)
@@ -904,11 +912,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
         if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
         if (!DET && tid == 0) s_ndl = 0;  // (published by the barrier after the quadrant tests)
+#if LGM_AB_NB
+        {  // every wave zeroes its own slot (an entry it skips, or never lists, adds nothing): no barrier needed
+            float4 *z = reinterpret_cast<float4 *>(myAcc);
+            for (int q = lane; q < SLOT / 4; q += 64) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#else
         {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
             static_assert((4 * LS * (NROW + 1)) % 4 == 0, "slot zeroing by float4");
             float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
             for (int q = tid; q < 4 * LS * (NROW + 1) / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
+#endif
         int cnt;
         {
             bool hit = false;
@@ -923,7 +938,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             constexpr int PAD = (int)(sizeof(S.list[0]) / sizeof(S.list[0][0])) - CH;
             if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)CH;
         }
-        __syncthreads();  // the zeroed slots (and the ids) before any flush
+        if (!LGM_AB_NB) __syncthreads();  // the zeroed slots (and the ids) before any flush
         if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
         id_cur = id_next;
         id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
@@ -1004,6 +1019,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         SEC_ADD(sec[2], ts_c1, ts_c2);  // the entries loop (evaluation, moments)
 #endif
         __syncthreads();
+#if LGM_AB_CONV
+        // moments -> gradient partials, an entry's three groups on three waves at once (thread 64 g + j, entry j):
+        // g = 0 mean2D + opacity (moment rows 0..2), g = 1 conic (rows 0..5; a needle's go to rows NV..NV+2 for the
+        // fp64 flush), g = 2 colour [+ depth] (the hi + lo rows). The partials go to wave 0's WU image (dead until
+        // the next chunk's entries loop, which starts after that chunk's first barrier), rows q * LS + j.
+        float *o = sWU[0];
+        if (w < 3 && b0 + lane < s1) {  // (w: wave-uniform)
+            const int j = lane;
+            auto msum = [&](int row) {
+                float v = 0.f;
+#pragma unroll
+                for (int ww = 0; ww < 4; ww++) v += sAccW[ww][row * LS + j];
+                return v;
+            };
+            if (w == 2) {
+#pragma unroll
+                for (int qq = 6; qq < NV; qq++) {
+                    float v = 0.f;
+#pragma unroll
+                    for (int ww = 0; ww < 4; ww++) v += sAccW[ww][qq * LS + j] + sAccW[ww][(qq + NC) * LS + j];
+                    o[qq * LS + j] = DET ? ldexpf(v, det_s) : v;
+                }
+            } else {
+                const float4 Pj = B.P[j];
+                const float4 Qj = B.Q[j];
+                float cA, cB, cC, op;  // the upstream conic and opacity
+                rec_conic(Pj, Qj, cA, cB, cC, op);
+                const float xg = Pj.x - cxT, yg = Pj.y - cyT;
+                const float q0 = msum(0), q1 = msum(1), q2 = msum(2);
+                DetNorm nm;
+                if (DET) nm = det_norm(Pj.z, Pj.w, Qj.x, d.W, d.H);
+                if (w == 0) {
+                    const float Sx = fmaf(xg, q0, -q1), Sy = fmaf(yg, q0, -q2);
+                    float p0 = -ddelx_dx * (cA * Sx + cB * Sy);
+                    float p1 = -ddely_dy * (cC * Sy + cB * Sx);
+                    float p5 = op > 0.f ? q0 / op : 0.f;
+                    if (DET) {
+                        p0 = ldexpf(p0, det_s + nm.k[0]);
+                        p1 = ldexpf(p1, det_s + nm.k[1]);
+                        p5 = ldexpf(p5, det_s);
+                    }
+                    o[0 * LS + j] = p0;
+                    o[1 * LS + j] = p1;
+                    o[5 * LS + j] = p5;
+                } else {
+                    const float q3 = msum(3), q4 = msum(4), q5 = msum(5);
+                    const float Sxx = fmaf(xg, fmaf(xg, q0, -2.f * q1), q3);
+                    const float Sxy = fmaf(xg, fmaf(yg, q0, -q2), fmaf(-yg, q1, q4));
+                    const float Syy = fmaf(yg, fmaf(yg, q0, -2.f * q2), q5);
+                    float pc[3] = {-0.5f * Sxx, -0.5f * Sxy, -0.5f * Syy};
+                    if (DET) {
+#pragma unroll
+                        for (int qq = 0; qq < 3; qq++) pc[qq] = ldexpf(pc[qq], det_s + nm.k[2 + qq]);
+                    }
+                    const bool ndl = !DET && rec_needle(Pj.z, Pj.w, Qj.x);
+#pragma unroll
+                    for (int qq = 0; qq < 3; qq++) {
+                        o[(2 + qq) * LS + j] = ndl ? 0.f : pc[qq];
+                        if (!DET) o[(NV + qq) * LS + j] = ndl ? pc[qq] : 0.f;
+                    }
+                    if (ndl) s_ndl = 1;  // (benign race: every writer stores 1)
+                }
+            }
+        }
+#else
+        float *o = sAccW[0];
         // moments -> gradient partials (one thread per staged entry): the sum over the four waves' slots,
         // converted, into wave 0's slots
         if (tid < CH && b0 + tid < s1) {
@@ -1026,7 +1107,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const float Sxx = fmaf(xg, fmaf(xg, q[0], -2.f * q[1]), q[3]);
             const float Sxy = fmaf(xg, fmaf(yg, q[0], -q[2]), fmaf(-yg, q[1], q[4]));
             const float Syy = fmaf(yg, fmaf(yg, q[0], -2.f * q[2]), q[5]);
-            float *o = sAccW[0];
             float part[NACC];
             part[0] = -ddelx_dx * (cA * Sx + cB * Sy);
             part[1] = -ddely_dy * (cC * Sy + cB * Sx);
@@ -1053,6 +1133,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #pragma unroll
             for (int qq = 0; qq < NV; qq++) o[qq * LS + j] = part[qq];
         }
+#endif
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c3);
         SEC_ADD(sec[3], ts_c2, ts_c3);  // barrier + moments -> partials
@@ -1072,7 +1153,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const int f = it * FT + ft;
             const int j = f / NACC, q = f - j * NACC;
             if (q < NV && j < CH && b0 + j < s1) {
-                const float a = sAccW[0][q * LS + j];
+                const float a = o[q * LS + j];
                 const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
                 const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
                 if (a != 0.f) {
@@ -1094,7 +1175,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             asm volatile("" : "+v"(tt));  // (recomputed here: lane indices hoisted out of the chunk loop spilled)
             for (; tt < 3 * CH; tt += 256) {  // (one pass at CH <= 85)
                 const int j = tt % CH, c3 = tt / CH;
-                const float a = sAccW[0][(NV + c3) * LS + j];
+                const float a = o[(NV + c3) * LS + j];
                 if (a != 0.f && b0 + j < s1) {
                     const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
                     // (the side block's offset recomputed here from the SGPR dims: a pointer hoisted out of the

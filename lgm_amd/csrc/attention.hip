@@ -249,16 +249,18 @@ template <int DT, int D>
 __global__ __launch_bounds__(256) void k_attn_delta(int B, int L, int H, const typename Ty<DT>::T *__restrict__ o,
                                                     const typename Ty<DT>::T *__restrict__ dout,
                                                     float *__restrict__ delta) {
-    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;  // (b, q, h)
+    // thread -> (b, h, q), q fastest: the delta row is written coalesced (with h fastest every wave scattered its 64
+    // floats over 16 rows of L: 25 -> ? us at 8 x 16 x 4096 rows); each thread still reads its own contiguous D-vector
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (long long)B * L * H) return;
-    const long long bq = idx / H;
-    const int h = (int)(idx - bq * H);
-    const int b = (int)(bq / L), qrow = (int)(bq - (long long)b * L);
-    const long long off = idx * D;
+    const long long bh = idx / L;
+    const int qrow = (int)(idx - bh * L);
+    const int b = (int)(bh / H), h = (int)(bh - (long long)b * H);
+    const long long off = (((long long)b * L + qrow) * H + h) * D;
     float s = 0.f;
 #pragma unroll 8
     for (int d = 0; d < D; d++) s += to_f(o[off + d]) * to_f(dout[off + d]);
-    delta[((long long)b * H + h) * L + qrow] = s;
+    delta[idx] = s;
 }
 
 // dQ: grid (ceil(L/64), B*H). dQ = scale * sum_k dS K with dS = P o (dP - delta), P = exp(scale S - lse).
@@ -689,7 +691,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
     };
     auto store_rows2 = [&](int buf) {
         ld_.store(Qs[buf], Os[buf], LDK);
-        if (tid < 64) { sl[buf][tid] = pl; sd[buf][tid] = pd; }
+        if (tid < 64) { sl[buf][tid] = -pl; sd[buf][tid] = -pd; }  // stored negated: the accumulator inits
     };
     load_rows2(0);
     store_rows2(0);
@@ -708,12 +710,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                 qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
                 orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
             }
-            // (the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i)
+            // (the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i, read as stored)
             f32x4 ainit, dinit;
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                ainit[i] = -sl[cur][16 * sub + 4 * g + i];
-                dinit[i] = -sd[cur][16 * sub + 4 * g + i];
+                ainit[i] = sl[cur][16 * sub + 4 * g + i];  // -lse' (negated when stored: no per-tile negations)
+                dinit[i] = sd[cur][16 * sub + 4 * g + i];  // -delta
             }
 #pragma unroll
             for (int s = 0; s < KS; s++) {

@@ -83,11 +83,8 @@ struct StageT {                                   // PAD: list padding = entries
 constexpr int FWD_FU = 4;
 using StageFwd = StageT<1, FWD_FU>;
 constexpr int BWD_CHUNK = 64;
-#ifndef LGM_AB_NB
-#define LGM_AB_NB 0  // (A/B in progress) 1: per-wave slot zeroing, no barrier between the quadrant tests and the entries
-#endif
-#ifndef LGM_AB_CONV
-#define LGM_AB_CONV 0  // (A/B in progress) 1: the moments -> partials conversion split over three waves
+#ifndef LGM_AB_HB
+#define LGM_AB_HB 0  // (A/B in progress) 1: a batch whose second half is padding evaluates only its first
 #endif
 // backward lists are padded to MB with the sentinel: every list position is one MFMA batch column (k_render_bwd)
 using StageBwd = StageT<2, MB, BWD_CHUNK>;
@@ -700,10 +697,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // moment rows: 0..5 geometric (w columns), then dL/dpixel-hi and dL/dpixel-lo sums of the NC colour [+ depth]
     // channels (u columns); row NROW is the junk row
     constexpr int NC = DEPTH ? 4 : 3, NROW = 6 + 2 * NC;
-    constexpr int SLOT = LGM_AB_NB ? (LS * (NROW + 1) + 3) & ~3 : LS * (NROW + 1);  // (NB: 16-B aligned slots)
+    constexpr int SLOT = (LS * (NROW + 1) + 3) & ~3;  // 16-B aligned slots (zeroed by float4)
     __shared__ __attribute__((aligned(16))) float sAccW[4][SLOT];
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
-    static_assert(!LGM_AB_CONV || (NV + 3) * LS <= 16 * WU_LD, "the partial rows fit wave 0's WU image");
+    static_assert((NV + 3) * LS <= 16 * WU_LD, "the partial rows fit wave 0's WU image");
     __shared__ int s_ndl;  // the chunk holds a needle-like record (its conic partials go to the fp64 side block)
 
     // ---- work item: (tile, chunk c, checkpoint slot)
@@ -911,19 +908,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         // one row per lane: every wave tests all CH entries against its OWN quadrant (one ellipse test per lane
         // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
         if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
-        if (!DET && tid == 0) s_ndl = 0;  // (published by the barrier after the quadrant tests)
-#if LGM_AB_NB
-        {  // every wave zeroes its own slot (an entry it skips, or never lists, adds nothing): no barrier needed
+        if (!DET && tid == 0) s_ndl = 0;  // (published by the barrier after the entries loop)
+        {  // every wave zeroes its own slot (an entry it skips, or never lists, adds nothing): wave-private, so the
+           // entries loop follows the quadrant tests without a barrier (with the conversion over three waves below:
+           // pool k_render_bwd 642 -> 635 us, bitwise equal, profiles/r04/ab_bwd_conv)
             float4 *z = reinterpret_cast<float4 *>(myAcc);
             for (int q = lane; q < SLOT / 4; q += 64) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
-#else
-        {  // every wave's slots start at zero (an entry a wave skips, or never lists, adds nothing)
-            static_assert((4 * LS * (NROW + 1)) % 4 == 0, "slot zeroing by float4");
-            float4 *z = reinterpret_cast<float4 *>(&sAccW[0][0]);
-            for (int q = tid; q < 4 * LS * (NROW + 1) / 4; q += 256) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#endif
         int cnt;
         {
             bool hit = false;
@@ -938,7 +929,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             constexpr int PAD = (int)(sizeof(S.list[0]) / sizeof(S.list[0][0])) - CH;
             if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)CH;
         }
-        if (!LGM_AB_NB) __syncthreads();  // the zeroed slots (and the ids) before any flush
         if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
         id_cur = id_next;
         id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
@@ -958,6 +948,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             list_raw<MB>(S, w, kk + MB, lraw);        // in bounds: the list rows hold kRows + MB words
 #pragma unroll
             for (int h = 0; h < 2; h++) {
+#if LGM_AB_HB
+                // the chunk's last batch often holds <= 4 listed entries: its second half (padding) is not
+                // evaluated; the stale w / u columns it leaves multiply into the sentinel column CH only
+                if (h == 1 && kk + 4 >= cnt) break;  // (wave-uniform)
+#endif
                 float al[4], Gw[4];
                 float4 cc[4], Pv[4], Qv[4];
 #pragma unroll
@@ -1019,7 +1014,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         SEC_ADD(sec[2], ts_c1, ts_c2);  // the entries loop (evaluation, moments)
 #endif
         __syncthreads();
-#if LGM_AB_CONV
         // moments -> gradient partials, an entry's three groups on three waves at once (thread 64 g + j, entry j):
         // g = 0 mean2D + opacity (moment rows 0..2), g = 1 conic (rows 0..5; a needle's go to rows NV..NV+2 for the
         // fp64 flush), g = 2 colour [+ depth] (the hi + lo rows). The partials go to wave 0's WU image (dead until
@@ -1083,57 +1077,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 }
             }
         }
-#else
-        float *o = sAccW[0];
-        // moments -> gradient partials (one thread per staged entry): the sum over the four waves' slots,
-        // converted, into wave 0's slots
-        if (tid < CH && b0 + tid < s1) {
-            const int j = tid;
-            const float4 Pj = B.P[j];
-            const float4 Qj = B.Q[j];
-            float cA, cB, cC, op;  // the upstream conic and opacity
-            rec_conic(Pj, Qj, cA, cB, cC, op);
-            const float xg = Pj.x - cxT, yg = Pj.y - cyT;
-            float q[NACC];
-#pragma unroll
-            for (int qq = 0; qq < NV; qq++) {  // (colour [depth] rows: the hi and the lo dL/dpixel sums)
-                float s = 0.f;
-#pragma unroll
-                for (int ww = 0; ww < 4; ww++)
-                    s += qq < 6 ? sAccW[ww][qq * LS + j] : sAccW[ww][qq * LS + j] + sAccW[ww][(qq + NC) * LS + j];
-                q[qq] = s;
-            }
-            const float Sx = fmaf(xg, q[0], -q[1]), Sy = fmaf(yg, q[0], -q[2]);
-            const float Sxx = fmaf(xg, fmaf(xg, q[0], -2.f * q[1]), q[3]);
-            const float Sxy = fmaf(xg, fmaf(yg, q[0], -q[2]), fmaf(-yg, q[1], q[4]));
-            const float Syy = fmaf(yg, fmaf(yg, q[0], -2.f * q[2]), q[5]);
-            float part[NACC];
-            part[0] = -ddelx_dx * (cA * Sx + cB * Sy);
-            part[1] = -ddely_dy * (cC * Sy + cB * Sx);
-            part[2] = -0.5f * Sxx;
-            part[3] = -0.5f * Sxy;
-            part[4] = -0.5f * Syy;
-            part[5] = op > 0.f ? q[0] / op : 0.f;
-#pragma unroll
-            for (int qq = 6; qq < NV; qq++) part[qq] = q[qq];
-            if (DET) {  // fixed-point units: the call's seed scale and the record's normalisers (exact powers of two)
-                const DetNorm nm = det_norm(Pj.z, Pj.w, Qj.x, d.W, d.H);
-#pragma unroll
-                for (int qq = 0; qq < NV; qq++) part[qq] = ldexpf(part[qq], det_s + (qq < 5 ? nm.k[qq] : 0));
-            }
-            if (!DET) {  // a needle's conic partials move to the (dead) lo rows NV.. for the fp64 flush
-                const bool ndl = rec_needle(Pj.z, Pj.w, Qj.x);
-#pragma unroll
-                for (int qq = 2; qq <= 4; qq++) {
-                    o[(NV + qq - 2) * LS + j] = ndl ? part[qq] : 0.f;
-                    part[qq] = ndl ? 0.f : part[qq];
-                }
-                if (ndl) s_ndl = 1;  // (benign race: every writer stores 1)
-            }
-#pragma unroll
-            for (int qq = 0; qq < NV; qq++) o[qq * LS + j] = part[qq];
-        }
-#endif
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c3);
         SEC_ADD(sec[3], ts_c2, ts_c3);  // barrier + moments -> partials

@@ -445,6 +445,10 @@ __device__ __forceinline__ typename Ty<DT>::V8 tr_frag(const typename Ty<DT>::T 
 // 2-way on both (SQ_LDS_BANK_CONFLICT = half of the forward's LDS cycles, profiles/r02/pmc_attn). Measured
 // (profiles/r02/ab_attn_pad): D = 64 fwd / dQ / dK,dV -5 / -8 / -10 %; D = 32 unchanged.
 constexpr int LDK_PAD = 16, FWD_WPE = 3, BWD_WPE = 2;
+// dK,dV at D = 32 with its tile in two 32-query halves (half the score registers live) held at 4 waves per SIMD (128
+// VGPRs; 3 at the compiler's own 136): bench level k_attn_dkdv 636 -> 625 us (profiles/r04/ab_session_f; the
+// forward split the same way ran 412 -> 435 us and stays whole)
+constexpr int DKDV_WPE32 = 4;
 // The softmax's affine parts ride on the MFMAs: the register operand (Q in the forward and dQ kernels, K in dK/dV)
 // is pre-scaled by scale * log2(e) (rounded to the 16-bit type once), so S comes out in log2 units, and the S / dP
 // accumulators start at -m (-lse') and -delta of their rows, so exp2's argument and dS's (dP - delta) factor leave
@@ -647,7 +651,7 @@ struct TileLoader {  // one 64-row tile of up to two [tokens][ld] tensors, CH 16
 
 // dK, dV: grid (ceil(L / (64 KS)), B*H); wavefront w owns keys k0 + 16 s + (lane & 15), s < KS.
 template <int DT, int D, int KS>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BWD_WPE : 1))) void k_attn_dkdv2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DKDV_WPE32 : D <= 64 ? BWD_WPE : 1))) void k_attn_dkdv2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
                                                    const typename Ty<DT>::T *__restrict__ k,
                                                    const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                    const typename Ty<DT>::T *__restrict__ dout,
@@ -701,59 +705,61 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         const bool more = qb + 64 < L;
         if (more) load_rows2(qb + 64);
         const T *Qt = Qs[cur], *Ot = Os[cur];
-        f32x4 sacc[KS][4], dpa[KS][4];
+        // the tile's two 32-query halves one after the other (S / dP of subs 2t, 2t + 1, then their dV / dK
+        // products): half the score registers live at once (dK,dV at D = 32 fits 4 waves per SIMD instead of 3)
 #pragma unroll
-        for (int sub = 0; sub < 4; sub++) {
-            V8 qr[D / 32], orr[D / 32];
+        for (int t = 0; t < 2; t++) {
+            f32x4 sacc[KS][2], dpa[KS][2];
 #pragma unroll
-            for (int cc = 0; cc < D / 32; cc++) {
-                qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
-                orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
-            }
-            // (the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i, read as stored)
-            f32x4 ainit, dinit;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                ainit[i] = sl[cur][16 * sub + 4 * g + i];  // -lse' (negated when stored: no per-tile negations)
-                dinit[i] = sd[cur][16 * sub + 4 * g + i];  // -delta
-            }
-#pragma unroll
-            for (int s = 0; s < KS; s++) {
-                f32x4 a = ainit, dp = dinit;
+            for (int h2 = 0; h2 < 2; h2++) {
+                const int sub = 2 * t + h2;
+                V8 qr[D / 32], orr[D / 32];
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
-                    a = mfma32<DT>(qr[cc], kf[s].v[cc], a);     // S[q = 16 sub + 4g + i][key]
-                    dp = mfma32<DT>(orr[cc], vf[s].v[cc], dp);  // dP[q][key]
+                    qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                    orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
                 }
-                sacc[s][sub] = a;
-                dpa[s][sub] = dp;
-            }
-        }
-        V8 pb[KS][2], db[KS][2];
+                // (the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i, read as stored)
+                f32x4 ainit, dinit;
 #pragma unroll
-        for (int sub = 0; sub < 4; sub++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
+                for (int i = 0; i < 4; i++) {
+                    ainit[i] = sl[cur][16 * sub + 4 * g + i];  // -lse' (negated when stored: no per-tile negations)
+                    dinit[i] = sd[cur][16 * sub + 4 * g + i];  // -delta
+                }
 #pragma unroll
                 for (int s = 0; s < KS; s++) {
-                    const float p = __builtin_amdgcn_exp2f(sacc[s][sub][i]);
-                    const float ds = p * dpa[s][sub][i];
-                    pb[s][sub >> 1][4 * (sub & 1) + i] = (T)p;
-                    db[s][sub >> 1][4 * (sub & 1) + i] = (T)ds;
+                    f32x4 a = ainit, dp = dinit;
+#pragma unroll
+                    for (int cc = 0; cc < D / 32; cc++) {
+                        a = mfma32<DT>(qr[cc], kf[s].v[cc], a);     // S[q = 16 sub + 4g + i][key]
+                        dp = mfma32<DT>(orr[cc], vf[s].v[cc], dp);  // dP[q][key]
+                    }
+                    sacc[s][h2] = a;
+                    dpa[s][h2] = dp;
                 }
             }
+            V8 pb[KS], db[KS];
 #pragma unroll
-        for (int t = 0; t < 2; t++)
+            for (int h2 = 0; h2 < 2; h2++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int s = 0; s < KS; s++) {
+                        const float p = __builtin_amdgcn_exp2f(sacc[s][h2][i]);
+                        pb[s][4 * h2 + i] = (T)p;
+                        db[s][4 * h2 + i] = (T)(p * dpa[s][h2][i]);
+                    }
 #pragma unroll
             for (int dt = 0; dt < D / 16; dt++) {
                 const V8 oT = tr_frag<DT>(Ot, LDK, 32 * t, 16 * dt, lane);  // dO^T
                 const V8 qT = tr_frag<DT>(Qt, LDK, 32 * t, 16 * dt, lane);  // Q^T
 #pragma unroll
                 for (int s = 0; s < KS; s++) {
-                    dva[s][dt] = mfma32<DT>(oT, pb[s][t], dva[s][dt]);
-                    dka[s][dt] = mfma32<DT>(qT, db[s][t], dka[s][dt]);
+                    dva[s][dt] = mfma32<DT>(oT, pb[s], dva[s][dt]);
+                    dka[s][dt] = mfma32<DT>(qT, db[s], dka[s][dt]);
                 }
             }
+        }
         if (more) store_rows2(cur ^ 1);
         __syncthreads();
         cur ^= 1;
@@ -823,49 +829,52 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         const bool more = kb + 64 < L;
         if (more) ld_.load(k + base, ld, v + base, ld, kb + 64, L);
         const T *Kt = Ks[cur], *Vt = Vs[cur];
-        f32x4 sacc[QS][4], dpa[QS][4];
+        // the tile's two 32-key halves one after the other (half the score registers live at once)
 #pragma unroll
-        for (int sub = 0; sub < 4; sub++) {
-            V8 kr[D / 32], vr[D / 32];
+        for (int t = 0; t < 2; t++) {
+            f32x4 sacc[QS][2], dpa[QS][2];
 #pragma unroll
-            for (int cc = 0; cc < D / 32; cc++) {
-                kr[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
-                vr[cc] = *reinterpret_cast<const V8 *>(Vt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
-            }
-#pragma unroll
-            for (int s = 0; s < QS; s++) {
-                // (the accumulators start at -lse' / -delta of the lane's query)
-                f32x4 a = {-l2[s], -l2[s], -l2[s], -l2[s]};
-                f32x4 dp = {-dl[s], -dl[s], -dl[s], -dl[s]};
+            for (int h2 = 0; h2 < 2; h2++) {
+                const int sub = 2 * t + h2;
+                V8 kr[D / 32], vr[D / 32];
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
-                    a = mfma32<DT>(kr[cc], qf[s].v[cc], a);    // S^T[key = 16 sub + 4g + i][q]
-                    dp = mfma32<DT>(vr[cc], of[s].v[cc], dp);  // dP^T[key][q]
+                    kr[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                    vr[cc] = *reinterpret_cast<const V8 *>(Vt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
                 }
-                sacc[s][sub] = a;
-                dpa[s][sub] = dp;
-            }
-        }
-        V8 db[QS][2];
-#pragma unroll
-        for (int sub = 0; sub < 4; sub++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const bool kv = !TAIL || kb + 16 * sub + 4 * g + i < L;
 #pragma unroll
                 for (int s = 0; s < QS; s++) {
-                    const float p = kv ? __builtin_amdgcn_exp2f(sacc[s][sub][i]) : 0.f;
-                    db[s][sub >> 1][4 * (sub & 1) + i] = (T)(p * dpa[s][sub][i]);
+                    // (the accumulators start at -lse' / -delta of the lane's query)
+                    f32x4 a = {-l2[s], -l2[s], -l2[s], -l2[s]};
+                    f32x4 dp = {-dl[s], -dl[s], -dl[s], -dl[s]};
+#pragma unroll
+                    for (int cc = 0; cc < D / 32; cc++) {
+                        a = mfma32<DT>(kr[cc], qf[s].v[cc], a);    // S^T[key = 16 sub + 4g + i][q]
+                        dp = mfma32<DT>(vr[cc], of[s].v[cc], dp);  // dP^T[key][q]
+                    }
+                    sacc[s][h2] = a;
+                    dpa[s][h2] = dp;
                 }
             }
+            V8 db[QS];
 #pragma unroll
-        for (int t = 0; t < 2; t++)
+            for (int h2 = 0; h2 < 2; h2++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const bool kv = !TAIL || kb + 32 * t + 16 * h2 + 4 * g + i < L;
+#pragma unroll
+                    for (int s = 0; s < QS; s++) {
+                        const float p = kv ? __builtin_amdgcn_exp2f(sacc[s][h2][i]) : 0.f;
+                        db[s][4 * h2 + i] = (T)(p * dpa[s][h2][i]);
+                    }
+                }
 #pragma unroll
             for (int dt = 0; dt < D / 16; dt++) {
                 const V8 kT = tr_frag<DT>(Kt, LDK, 32 * t, 16 * dt, lane);  // K^T
 #pragma unroll
-                for (int s = 0; s < QS; s++) dqa[s][dt] = mfma32<DT>(kT, db[s][t], dqa[s][dt]);
+                for (int s = 0; s < QS; s++) dqa[s][dt] = mfma32<DT>(kT, db[s], dqa[s][dt]);
             }
+        }
         if (more) ld_.store(Ks[cur ^ 1], Vs[cur ^ 1], LDK);
         __syncthreads();
         cur ^= 1;

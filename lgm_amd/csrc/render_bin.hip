@@ -51,7 +51,6 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 // per workgroup instead of once per view (pool 199 -> 193 us, single scene 40.6 -> 38.8 us; 1 / 2 / 6 views per
 // workgroup measured slower).
 constexpr int BIN_THREADS = 512, BIN_G = BIN_THREADS, BIN_ITERS = 3;
-static_assert(BIN_G == BIN_SEG, "a binning workgroup's segment of a tile slot");
 constexpr int BIN_HITCAP = BIN_THREADS * 6;  // hit-list capacity (typical: ~4 hits per Gaussian)
 static_assert(BIN_THREADS <= 512, "owner index packs into 9 bits");
 
@@ -121,8 +120,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                                                      int *__restrict__ tile_count, const int *__restrict__ tile_start,
                                                      unsigned long long *__restrict__ pairs, long long slot_stride,
                                                      unsigned long long *__restrict__ misc, float *__restrict__ accum,
-                                                     int *__restrict__ corder, int *__restrict__ cntrow,
-                                                     unsigned *__restrict__ mzero) {
+                                                     int *__restrict__ corder) {
     extern __shared__ int hist[];  // [T] per-tile hit counts, [T] reserved global bases, [T] fallback cursors
     __shared__ BinRec srec[BIN_THREADS];
     __shared__ int sHead[BIN_THREADS], sExcl[BIN_THREADS];
@@ -138,9 +136,6 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     int *hbase = hist + T, *fill = hist + 2 * T;
     int *cur = tile_count + (size_t)bv * T;
     if (tid < 2) s_tot[tid] = 0;
-    // (count-row mode: no memset precedes the launch; the later kernels' counters -- checkpoint regions, the fused
-    // loss's arrival counter, the deterministic saturation count -- are zeroed here, by one workgroup)
-    if (mzero && blockIdx.x == 0 && blockIdx.y == 0 && tid < 10) mzero[tid] = 0u;
     auto dest = [&](int t, int pos) -> long long {
         return (MODE == EMIT_SLOT ? ((long long)bv * T + t) * slot_stride
                                   : (long long)tile_start[(size_t)bv * T + t]) + pos;
@@ -306,22 +301,13 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
     if (lds) {
         __syncthreads();
         phase(1);
-        if (MODE == EMIT_SLOT && cntrow) {  // this workgroup's segment of every tile slot; its counts as a row
-            int *row = cntrow + ((size_t)bv * gridDim.x + blockIdx.x) * T;
-            for (int t = tid; t < T; t += BIN_THREADS) {
-                row[t] = hist[t];
-                hbase[t] = (int)blockIdx.x * BIN_G;
-                fill[t] = 0;
+        for (int t = tid; t < T; t += BIN_THREADS) {
+            const int c = hist[t];
+            if (c) {
+                if (MODE == COUNT) atomicAdd(&cur[t], c);
+                else hbase[t] = atomicAdd(&cur[t], c);
             }
-        } else {
-            for (int t = tid; t < T; t += BIN_THREADS) {
-                const int c = hist[t];
-                if (c) {
-                    if (MODE == COUNT) atomicAdd(&cur[t], c);
-                    else hbase[t] = atomicAdd(&cur[t], c);
-                }
-                fill[t] = 0;
-            }
+            fill[t] = 0;
         }
         __syncthreads();
         phase(2);
@@ -350,7 +336,7 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
         stamp[7] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
     }
     }  // batches
-    if (tid == 0 && misc) {  // (pair totals: only when the caller asked for them)
+    if (tid == 0) {
         atomicAdd(&misc[0], s_tot[0]);
         atomicAdd(&misc[1], s_tot[1]);
     }
@@ -397,15 +383,6 @@ __global__ __launch_bounds__(1024) void k_scan(const int *__restrict__ count, in
 // RS_CAP is 4032, not 4096: the workgroup's whole LDS (the dynamic image, RS_CAP * 8 + 8 KB on the MSD path, plus
 // ~400 B of static __shared__) must stay <= 40 KB for 4 workgroups per CU (160 KB). At 4096 it was 41,360 B and
 // the kernel ran 3 per CU; lists of 4033..4096 entries now take the (rare) oversized path.
-#ifndef LGM_AB_PRIV
-#define LGM_AB_PRIV 0  // (A/B in progress) 1: per-workgroup count rows instead of zeroed counters + reservations
-#endif
-#if LGM_AB_PRIV && LGM_AB_SPAIR
-#error "LGM_AB_PRIV and LGM_AB_SPAIR are separate A/B arms"
-#endif
-#ifndef LGM_AB_SPAIR
-#define LGM_AB_SPAIR 0  // (A/B in progress) 1: two small tiles per sort workgroup
-#endif
 constexpr int RS_THREADS = 512, RS_WAVES = RS_THREADS / 64, RS_CAP = 4032,
               RS_MAXR = (RS_CAP + RS_THREADS - 1) / RS_THREADS;
 constexpr int RS_OBLK = 4096;  // sort_oversized's LDS block (a power of two), u64 keys over the image
@@ -595,17 +572,12 @@ __device__ void sort_oversized(unsigned long long *seg, int n, unsigned long lon
 constexpr int MSD_BITS = 11, MSD_B = 1 << MSD_BITS, MSD_LIMIT = 48;
 static_assert(MSD_B % RS_THREADS == 0, "scan layout");
 
-// NT threads (tid: the thread's index in its group, 0..NT-1) sort one tile on NBITS-bit buckets; the flag *s_flag
-// is shared by every group of the workgroup (so all of them leave or stay together: the barriers are the
-// workgroup's).
-template <int NT = RS_THREADS, int NBITS = MSD_BITS>
 __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const unsigned (&ir)[RS_MAXR], int n,
                                          int c0, int R, int kbits, unsigned *sk, unsigned *hc, int *s_wsum,
-                                         int *s_flag, unsigned *__restrict__ ids_out, int tid = threadIdx.x) {
-    const int w = tid >> 6, lane = tid & 63;
-    const int shift = kbits > NBITS ? kbits - NBITS : 0;
-    constexpr int BPT = (1 << NBITS) / NT;
-    static_assert((1 << NBITS) % NT == 0, "scan layout");
+                                         int *s_flag, unsigned *__restrict__ ids_out) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int shift = kbits > MSD_BITS ? kbits - MSD_BITS : 0;
+    constexpr int BPT = MSD_B / RS_THREADS;
     // (hc and *s_flag were zeroed by sort_tile under its span barrier)
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
@@ -647,7 +619,7 @@ __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const un
         }
     }
     __syncthreads();
-    for (int q = tid; q < n; q += NT) {
+    for (int q = tid; q < n; q += RS_THREADS) {
         const unsigned long long cq = skv[q];
         const unsigned bq = (unsigned)(cq >> 32) >> shift;
         const int lo = bq ? (int)hc[bq - 1] : 0, hi = (int)hc[bq];
@@ -659,52 +631,15 @@ __device__ __forceinline__ bool msd_sort(const unsigned (&kr)[RS_MAXR], const un
 }
 
 // One tile's bucket: LDS LSD radix sort (see the file header); all threads of the block call it.
-// Count-row mode (segP != null): the tile's entries lie in G segments of its slot -- segment g (binning workgroup g)
-// at g * BIN_SEG, segP[g] entries before it in the list order (segP: exclusive prefix in LDS, at the start of the sort
-// image, dead once the entries are loaded) -- and are gathered from there: entry e of the list is at src(e). A path
-// that re-reads the list by position (the LSD and tie paths, sort_oversized) first writes it back contiguous.
-__device__ __forceinline__ int seg_src(const int *segP, int G, int e) {
-    int lo = 0, len = G;  // the last segment g with segP[g] <= e (an empty segment's successor starts at the same e)
-    while (len > 1) {
-        const int h = len >> 1;
-        lo = segP[lo + h] <= e ? lo + h : lo;
-        len -= h;
-    }
-    return lo * BIN_SEG + (e - segP[lo]);
-}
-__device__ __forceinline__ void sort_tile(long long base, int n, unsigned long long *__restrict__ pairs,
-                                          const int *segP = nullptr, int G = 0) {
+__device__ __forceinline__ void sort_tile(long long base, int n, unsigned long long *__restrict__ pairs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned *sk = reinterpret_cast<unsigned *>(smem);
     unsigned short *sp = reinterpret_cast<unsigned short *>(sk + RS_CAP);
     RsCnt *cnt = reinterpret_cast<RsCnt *>(sp + RS_CAP);
     __shared__ unsigned s_vmax;
     __shared__ int s_wsum[RS_WAVES], s_long, s_flag;
+    if (n <= 1) return;  // a single id already sits in place (low half of its key)
     unsigned long long *seg = pairs + base;
-    if (segP && n > RS_CAP) {  // gathered contiguous first, in passes of RS_MAXR * RS_THREADS entries: an entry's
-        // destination e never exceeds its source, nor any later entry's source, so a pass may overwrite only what
-        // earlier passes have read
-        for (int c = 0; c < n; c += RS_MAXR * RS_THREADS) {
-            unsigned long long v[RS_MAXR];
-#pragma unroll
-            for (int r = 0; r < RS_MAXR; r++) {
-                const int e = c + r * RS_THREADS + (int)threadIdx.x;
-                if (e < n) v[r] = seg[seg_src(segP, G, e)];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < RS_MAXR; r++) {
-                const int e = c + r * RS_THREADS + (int)threadIdx.x;
-                if (e < n) seg[e] = v[r];
-            }
-            __syncthreads();
-        }
-        segP = nullptr;
-    }
-    if (n <= 1) {  // a single id: in place (low half of its key), or moved to the front from its segment
-        if (segP && n == 1 && threadIdx.x == 0) reinterpret_cast<unsigned *>(seg)[0] = (unsigned)seg[seg_src(segP, G, 0)];
-        return;
-    }
     if (n > RS_CAP) {
         sort_oversized(seg, n, reinterpret_cast<unsigned long long *>(smem));
         return;
@@ -721,7 +656,7 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
         const int e = c0 + r * 64 + lane;
-        if (r < R) xv[r] = seg[segP ? seg_src(segP, G, min(e, n - 1)) : min(e, n - 1)];  // (r < R: uniform)
+        if (r < R) xv[r] = seg[min(e, n - 1)];  // (r < R is workgroup-uniform)
     }
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) {
@@ -775,15 +710,6 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     if (kbits > 0 && msd_sort(kr, ir, n, c0, R, kbits, sk, reinterpret_cast<unsigned *>(smem) + 2 * RS_CAP, s_wsum,
                               &s_flag, reinterpret_cast<unsigned *>(seg)))
         return;
-    if (segP) {  // the paths below re-read the list by position: contiguous from here (every load is done: the
-                 // span barrier above followed them)
-#pragma unroll
-        for (int r = 0; r < RS_MAXR; r++) {
-            const int e = c0 + r * 64 + lane;
-            if (r < R && e < n) seg[e] = ((unsigned long long)(kr[r] + kmin) << 32) | ir[r];
-        }
-        __syncthreads();
-    }
     unsigned idr[RS_MAXR];
 #pragma unroll
     for (int r = 0; r < RS_MAXR; r++) pr[r] = (unsigned short)(c0 + r * 64 + lane);  // bucket positions
@@ -880,74 +806,13 @@ __device__ __forceinline__ void sort_tile(long long base, int n, unsigned long l
     }
 }
 
-#if LGM_AB_SPAIR
-// Two small tiles in one workgroup (both lists <= SP_CAP): each half (256 threads, 4 waves) runs the MSD sort of
-// its tile in its own half of the LDS image (SP_CAP u64 entries + 2^SP_BITS u32 bucket counters), the two halves
-// in lockstep through the workgroup's barriers. Returns false -- nothing written -- when either tile needs more than
-// one MSD pass (a bucket over MSD_LIMIT, or equal keys only): the caller then sorts both tiles one after the other.
-constexpr int SP_THREADS = RS_THREADS / 2, SP_BITS = MSD_BITS - 1, SP_CAP = 2016;
-static_assert(2 * (SP_CAP * 8 + (1 << SP_BITS) * 4) <= RS_LDS, "two halves in the sort image");
-static_assert((SP_CAP + SP_THREADS - 1) / SP_THREADS <= RS_MAXR, "rows per lane");
-__device__ __forceinline__ bool sort_pair(long long base0, int n0, long long base1, int n1,
-                                          unsigned long long *__restrict__ pairs) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ unsigned s_pmm[2][2][SP_THREADS / 64];
-    __shared__ int s_pw[2][SP_THREADS / 64], s_pflag;
-    const int tid = threadIdx.x, half = tid / SP_THREADS, gt = tid - half * SP_THREADS, w = gt >> 6, lane = tid & 63;
-    unsigned *sk = reinterpret_cast<unsigned *>(smem + half * (SP_CAP * 8 + (1 << SP_BITS) * 4));
-    unsigned *hc = sk + 2 * SP_CAP;
-    const int n = half ? n1 : n0;
-    unsigned long long *seg = pairs + (half ? base1 : base0);
-    const int C = ((n + SP_THREADS - 1) / SP_THREADS) * 64, R = C >> 6, c0 = w * C;
-    unsigned kr[RS_MAXR], ir[RS_MAXR];
-    unsigned long long xv[RS_MAXR];
-#pragma unroll
-    for (int r = 0; r < RS_MAXR; r++) {
-        const int e = c0 + r * 64 + lane;
-        if (r < R) xv[r] = seg[min(e, n - 1)];  // (r < R is uniform per half; R = 0 for an empty tile)
-    }
-    unsigned lmin = 0xffffffffu, lmax = 0u;
-#pragma unroll
-    for (int r = 0; r < RS_MAXR; r++) {
-        kr[r] = 0u;
-        ir[r] = 0u;
-        const int e = c0 + r * 64 + lane;
-        if (r < R && e < n) {
-            kr[r] = (unsigned)(xv[r] >> 32);
-            ir[r] = (unsigned)xv[r];
-            lmin = min(lmin, kr[r]);
-            lmax = max(lmax, kr[r]);
-        }
-    }
-    if (tid == 0) s_pflag = 0;
-    for (int q = gt; q < (1 << SP_BITS); q += SP_THREADS) hc[q] = 0u;
-    lmin = wave_min_u32(lmin);
-    lmax = wave_max_u32(lmax);
-    if (lane == 0) { s_pmm[half][0][w] = lmin; s_pmm[half][1][w] = lmax; }
-    __syncthreads();
-    unsigned kmin = s_pmm[half][0][0], kmax = s_pmm[half][1][0];
-#pragma unroll
-    for (int ww = 1; ww < SP_THREADS / 64; ww++) {
-        kmin = min(kmin, s_pmm[half][0][ww]);
-        kmax = max(kmax, s_pmm[half][1][ww]);
-    }
-    const unsigned span = n >= 2 ? kmax - kmin : 0u;
-    const int kbits = span ? 32 - __clz(span) : 0;
-    if (n >= 2 && kbits == 0 && gt == 0) s_pflag = 1;  // all keys equal: the id-order path (read after 2 barriers)
-#pragma unroll
-    for (int r = 0; r < RS_MAXR; r++) kr[r] -= kmin;
-    return msd_sort<SP_THREADS, SP_BITS>(kr, ir, n, c0, R, kbits, sk, hc, s_pw[half], &s_pflag,
-                                         reinterpret_cast<unsigned *>(seg), gt);
-}
-#endif
-
 // k_sort: grid (B*V*T), block RS_THREADS, dynamic LDS RS_LDS bytes; workgroup b sorts tile xcd_item(b), or with
 // the centre-first table (center_order) tile corder[b / BV] of view b % BV. 8 waves per SIMD: <= 64 VGPRs, 4
 // workgroups per CU with the u16 counters.
 __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8))) void k_sort(
-    int M, long long slot_stride, const int *__restrict__ tile_start, int *__restrict__ tile_count,
+    int M, long long slot_stride, const int *__restrict__ tile_start, const int *__restrict__ tile_count,
     unsigned long long *__restrict__ pairs, unsigned long long *__restrict__ counters, int BV, int T,
-    const int *__restrict__ corder, const int *__restrict__ cntrow, int G) {
+    const int *__restrict__ corder) {
     int tile = xcd_item(blockIdx.x, M);
     if (corder) {  // centre-first, views interleaved (center_order)
         const int r = (int)blockIdx.x / BV, v = (int)blockIdx.x - r * BV;
@@ -955,75 +820,13 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8)))
     }
     long long base;
     int n;
-    const int *segP = nullptr;
-    if (cntrow) {  // count-row mode: the G binning workgroups' counts of this tile -> exclusive prefix in LDS
-        extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-        __shared__ int s_sc[RS_WAVES];
-        int *sP = reinterpret_cast<int *>(smem);  // (the sort image's head: dead once sort_tile has loaded the list)
-        const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-        const int bv = tile / T, t = tile - bv * T;
-        int run = 0;
-        for (int g0 = 0; g0 < G; g0 += RS_THREADS) {
-            const int g = g0 + tid;
-            const int c = g < G ? cntrow[((size_t)bv * G + g) * T + t] : 0;
-            const int incl = wave_incl_scan(c, lane);
-            if (lane == 63) s_sc[w] = incl;
-            __syncthreads();
-            int pre = run, tot = 0;
-#pragma unroll
-            for (int ww = 0; ww < RS_WAVES; ww++) {
-                const int x = s_sc[ww];
-                pre += ww < w ? x : 0;
-                tot += x;
-            }
-            if (g < G) sP[g] = pre + incl - c;
-            run += tot;
-            __syncthreads();  // (s_sc reused by the next pass; sP complete for sort_tile)
-        }
-        n = run;
-        base = (long long)tile * slot_stride;
-        if (tid == 0) tile_count[tile] = n;  // for the compositing kernels (tile_range)
-        segP = sP;
-    } else {
-        tile_range(tile, slot_stride, tile_start, tile_count, base, n);
-    }
-#if LGM_AB_SPAIR
-    // workgroups b and b ^ 1 (in the same order) pair up when both lists are small: the even one sorts both tiles,
-    // the odd one leaves at once (both read the same two counts, so they agree)
-    int tile2 = -1, n2 = 0;
-    long long base2 = 0;
-    if ((blockIdx.x ^ 1u) < (unsigned)M) {
-        const int b2 = (int)(blockIdx.x ^ 1u);
-        tile2 = corder ? (b2 % BV) * T + corder[b2 / BV] : xcd_item(b2, M);
-        tile_range(tile2, slot_stride, tile_start, tile_count, base2, n2);
-    }
-    const bool paired = tile2 >= 0 && n <= SP_CAP && n2 <= SP_CAP;
-    if (paired && (blockIdx.x & 1u)) return;
-#endif
+    tile_range(tile, slot_stride, tile_start, tile_count, base, n);
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     if (counters && threadIdx.x == 0) {  // per-workgroup timeline + bucket size (see lgm_diag.render_counters)
         counters[8 + 8 * (size_t)tile + 4] = t_start;
         counters[8 + 8 * (size_t)tile + 6] = (unsigned long long)n;
     }
-#if LGM_AB_SPAIR
-    if (paired && counters && threadIdx.x == 0) {
-        counters[8 + 8 * (size_t)tile2 + 4] = t_start;
-        counters[8 + 8 * (size_t)tile2 + 6] = (unsigned long long)n2;
-    }
-    // (one inlined copy of sort_tile: the full path for a lone tile, or for both of a pair that the MSD pass could
-    // not finish -- workgroup-uniform)
-    const int reps = paired ? (sort_pair(base, n, base2, n2, pairs) ? 0 : 2) : 1;
-    for (int k = 0; k < reps; k++) {
-        __syncthreads();
-        sort_tile(k ? base2 : base, k ? n2 : n, pairs);
-    }
-    if (paired && counters) {
-        __syncthreads();
-        if (threadIdx.x == 0) counters[8 + 8 * (size_t)tile2 + 5] = __builtin_amdgcn_s_memrealtime();
-    }
-#else
-    sort_tile(base, n, pairs, segP, G);
-#endif
+    sort_tile(base, n, pairs);
     if (counters) {
         __syncthreads();
         if (threadIdx.x == 0) counters[8 + 8 * (size_t)tile + 5] = __builtin_amdgcn_s_memrealtime();
@@ -1037,15 +840,8 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                    char *ws, const Layout &L, int *radii_out, long long *stats_out, bool count_only,
                    hipStream_t st) {
     const size_t M = (size_t)d.BV * d.T;
-    const bool lds_hist = d.T <= LDS_HIST_MAX;
-    // count-row mode (slot workspace, LDS histogram): the binning writes per-workgroup tile counts and k_sort sums
-    // them, so no zeroed counters are needed -- no memset launch ahead of the binning (only the 16 B of pair totals
-    // when the caller asks for them)
-    const bool rows = LGM_AB_PRIV && L.slot && lds_hist && !count_only && d.N > 0 &&
-                      (d.N + BIN_G - 1) / BIN_G <= 2 * RS_CAP - 1;
     // tile counters and the misc counters are adjacent in the layout: one memset
-    const size_t zbytes = rows ? (stats_out ? 16 : 0) : L.misc + 64 - L.tile_count;
-    if (zbytes && hipMemsetAsync(ws + (rows ? L.misc : L.tile_count), 0, zbytes, st) != hipSuccess) {
+    if (hipMemsetAsync(ws + L.tile_count, 0, L.misc + 64 - L.tile_count, st) != hipSuccess) {
         set_error("hipMemsetAsync failed");
         return LGM_E_HIP;
     }
@@ -1054,9 +850,7 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     int *tcount = (int *)(ws + L.tile_count), *tstart = (int *)(ws + L.tile_start);
     unsigned long long *pairs = (unsigned long long *)(ws + L.pairs), *misc = (unsigned long long *)(ws + L.misc);
     float *accum = (float *)(ws + L.accum);
-    const size_t lds = lds_hist ? 3 * (size_t)d.T * 4 : 0;
-    int *cntrow = rows ? (int *)(ws + L.cntrow) : nullptr;
-    unsigned *mzero = rows ? (unsigned *)(ws + L.misc) + 4 : nullptr;
+    const size_t lds = d.T <= LDS_HIST_MAX ? 3 * (size_t)d.T * 4 : 0;
     // k_sort's centre-first tile table (the first T ints of the order buffer; the binning histogram's 3T ints of LDS
     // hold its counting sort)
     int *corder = lds && d.T >= 8 ? (int *)(ws + L.order) : nullptr;
@@ -1064,13 +858,12 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     if (d.N > 0) {
         if (count_only || !L.slot) {
             LGM_LAUNCH("k_bin_count", st, (k_bin<COUNT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
-                       gP, gQ, rects, nullptr, tcount, tstart, pairs, 0, misc, accum, nullptr, nullptr, nullptr)));
+                       gP, gQ, rects, nullptr, tcount, tstart, pairs, 0, misc, accum, nullptr)));
         }
         if (!count_only) {
             if (L.slot) {
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_SLOT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
-                           gP, gQ, rects, radii_out, tcount, tstart, pairs, (long long)d.N,
-                           rows && !stats_out ? nullptr : misc, accum, corder, cntrow, mzero)));
+                           gP, gQ, rects, radii_out, tcount, tstart, pairs, (long long)d.N, misc, accum, corder)));
             } else {
                 LGM_LAUNCH("k_scan", st, (k_scan<<<1, 1024, 0, st>>>(tcount, (int)M, tstart)));
                 if (hipMemsetAsync(ws + L.tile_count, 0, L.misc + 64 - L.tile_count, st) != hipSuccess) {
@@ -1078,12 +871,11 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
                     return LGM_E_HIP;
                 }
                 LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view,
-                           cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum, corder,
-                           nullptr, nullptr)));
+                           cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum, corder)));
             }
             LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M, RS_THREADS, RS_LDS, st>>>(
                                          (int)M, L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs, d.counters,
-                                         d.BV, d.T, corder, cntrow, (int)grid.x)));
+                                         d.BV, d.T, corder)));
         }
     }
     if (d.N == 0 && !L.slot && hipMemsetAsync(ws + L.tile_start, 0, (M + 1) * 4, st) != hipSuccess) {

@@ -34,7 +34,6 @@ constexpr int LDS_HIST_MAX = 8192;                   // tiles per view for the L
 constexpr float LOG2E = 1.4426950408889634f;
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
-constexpr int BIN_SEG = 512;  // Gaussians per binning workgroup (k_bin's BIN_G): its segment of a tile's slot
 // Deterministic mode takes no backward checkpoints: one backward work item per tile, so how a tile's walk splits into
 // work items cannot depend on which tiles won the shared pool's slot counters (a racing split changes the backward's
 // per-chunk partials in their last bits). A per-tile checkpoint quota was measured (profiles/r03/ab_det):
@@ -53,8 +52,7 @@ constexpr float ACC_NEEDLE = 300.0f;  // conic condition above which a record's 
 //   slot mode   (pair_capacity <= 0): tile (bv, t) owns pairs[(bv*T + t) * N, +N): no counting pass, no scan.
 //   packed mode (pair_capacity  > 0): tiles are packed by an exclusive scan of exact counts.
 struct Layout {
-    size_t gP, gQ, rects, tile_count, tile_start, order, cntrow, pairs, final_T, n_contrib, wlast, cfin, ck, cklist,
-        nck, cmask,
+    size_t gP, gQ, rects, tile_count, tile_start, order, pairs, final_T, n_contrib, wlast, cfin, ck, cklist, nck, cmask,
         accum, lossp, lossw, detmax, misc, total;
     long long cap;
     int ck_region;  // backward checkpoint slots per region (8 regions; the forward shards tiles over them)
@@ -81,10 +79,6 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
                         // fused loss reduction's arrival counter; u32 [13]: deterministic mode's saturated flushes)
     L.tile_start = take((BV * T + 1) * 4);
     L.order = take(T * 4);  // k_sort's centre-first tile table (center_order)
-    // slot mode: every binning workgroup's per-tile hit counts, [view][workgroup][tile] (k_bin -> k_sort): a
-    // workgroup's hits of tile t sit at its own segment (workgroup * BIN_SEG) of the tile's slot, so the binning
-    // needs no zeroed global counters and no reservation atomics; k_sort gathers the segments and writes the count
-    L.cntrow = L.slot ? take(BV * (size_t)((N + BIN_SEG - 1) / BIN_SEG) * T * 4) : 0;
     L.pairs = take((size_t)L.cap * 8);
     L.final_T = take(BV * P * 4);
     L.n_contrib = take(BV * P * 4);

@@ -83,9 +83,6 @@ struct StageT {                                   // PAD: list padding = entries
 constexpr int FWD_FU = 4;
 using StageFwd = StageT<1, FWD_FU>;
 constexpr int BWD_CHUNK = 64;
-#ifndef LGM_AB_HB
-#define LGM_AB_HB 0  // (A/B in progress) 1: a batch whose second half is padding evaluates only its first
-#endif
 // backward lists are padded to MB with the sentinel: every list position is one MFMA batch column (k_render_bwd)
 using StageBwd = StageT<2, MB, BWD_CHUNK>;
 
@@ -948,11 +945,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             list_raw<MB>(S, w, kk + MB, lraw);        // in bounds: the list rows hold kRows + MB words
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-#if LGM_AB_HB
-                // the chunk's last batch often holds <= 4 listed entries: its second half (padding) is not
-                // evaluated; the stale w / u columns it leaves multiply into the sentinel column CH only
+                // a batch with <= 4 listed entries (often a chunk's last) skips its second half, all padding: the
+                // stale w / u columns it leaves multiply into the sentinel column CH only (pool k_render_bwd 634 ->
+                // 614 us, bitwise equal: profiles/r04/ab_session_f)
                 if (h == 1 && kk + 4 >= cnt) break;  // (wave-uniform)
-#endif
                 float al[4], Gw[4];
                 float4 cc[4], Pv[4], Qv[4];
 #pragma unroll

@@ -20,12 +20,26 @@ python -c "
 import json
 for l in open('gpurun_out/attn_r4f.jsonl'):
     r=json.loads(l); print(r['level'], 'fwd %.0f TF fwdbwd %.0f TF' % (r['fwd_tflops'], r['fwdbwd_tflops']), {k: round(v, 3) for k, v in r['kernels_ms'].items()})"
-for v in base hb spair priv; do step hash_$v; LGM_AMD_LIB=$V/lib_$v.so timeout -k 10 120 python scripts/render_hashes.py 2>/dev/null | tail -1 > gpurun_out/hash_$v.json || exit $?; cat gpurun_out/hash_$v.json; done
+for v in base hb spair priv bin448 priv448; do step hash_$v; LGM_AMD_LIB=$V/lib_$v.so timeout -k 10 120 python scripts/render_hashes.py 2>/dev/null | tail -1 > gpurun_out/hash_$v.json || exit $?; cat gpurun_out/hash_$v.json; done
 rc=0
-for v in hb spair priv; do
+for v in hb spair priv priv448; do
   step tests_$v
   LGM_AMD_LIB=$V/lib_$v.so timeout -k 10 420 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_render_parity_gpu.py tests/test_render_gpu.py tests/test_loss_gpu.py > gpurun_out/t_$v.log 2>&1
   r=$?; tail -2 gpurun_out/t_$v.log; [ $r -eq 0 ] || [ $r -eq 1 ] || exit $r; rc=$((rc | r))
 done
-for r in 1 2 3; do for v in base hb spair priv; do step "ab $v r$r"; ab $v $r || exit $?; done; done
+for r in 1 2 3; do for v in base hb spair priv bin448 priv448; do step "ab $v r$r"; ab $v $r || exit $?; done; done
+# (3) attention: the tile bodies split into two 32-key / 32-query halves (asplit), and dK,dV held at 4 waves per
+# SIMD (asplit4), against abase (HEAD)
+for r in 1 2; do for v in abase asplit asplit4; do
+  step "attn $v r$r"; LGM_AMD_LIB=$V/lib_$v.so timeout -k 10 200 python scripts/bench_attn.py --no-sdpa --iters 20 > gpurun_out/attn_${v}_r$r.jsonl 2>/dev/null || exit $?
+  python -c "
+import json
+for l in open('gpurun_out/attn_${v}_r$r.jsonl'):
+    r=json.loads(l); print('$v', r['level'], 'fwd %.0f fwdbwd %.0f' % (r['fwd_tflops'], r['fwdbwd_tflops']), {k: round(v, 3) for k, v in r['kernels_ms'].items()})"
+done; done
+for v in asplit asplit4; do
+  step tests_$v
+  LGM_AMD_LIB=$V/lib_$v.so timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_attention.py -m gpu > gpurun_out/t_$v.log 2>&1
+  r=$?; tail -2 gpurun_out/t_$v.log; [ $r -eq 0 ] || [ $r -eq 1 ] || exit $r; rc=$((rc | r))
+done
 exit $((ra | rc))

@@ -50,9 +50,6 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 // A workgroup's BIN_ITERS batches are BIN_ITERS VIEWS of the same BIN_G Gaussians: each Gaussian row is loaded once
 // per workgroup instead of once per view (pool 199 -> 193 us, single scene 40.6 -> 38.8 us; 1 / 2 / 6 views per
 // workgroup measured slower).
-#ifndef LGM_AB_HIST4
-#define LGM_AB_HIST4 0  // (A/B in progress) 1: a row's LDS rank atomics issued four at a time
-#endif
 constexpr int BIN_THREADS = 512, BIN_G = BIN_THREADS, BIN_ITERS = 3;
 constexpr int BIN_HITCAP = BIN_THREADS * 6;  // hit-list capacity (typical: ~4 hits per Gaussian)
 static_assert(BIN_THREADS <= 512, "owner index packs into 9 bits");
@@ -279,26 +276,6 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
             int slot0 = 0;
             if (MODE != COUNT && lane == 0) slot0 = atomicAdd(&s_nhit, htot);
             slot0 = __builtin_amdgcn_readlane(slot0, 0) + hincl - cnt;
-#if LGM_AB_HIST4
-            // the row's hits four at a time: their LDS rank atomics issued together, one wait for the four returns
-            // (one atomic round trip per hit was a serial chain of LDS latencies)
-            for (int k0 = 0; k0 < cnt; k0 += 4) {
-                int rk[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (k0 + u < cnt) rk[u] = atomicAdd(&hist[trow + ta + k0 + u], 1);
-                if (MODE != COUNT) {
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const int slot = slot0 + k0 + u;
-                        if (k0 + u < cnt && slot < BIN_HITCAP) {
-                            sHit[slot] = (unsigned)owner | ((unsigned)(trow + ta + k0 + u) << 9);
-                            sRank[slot] = (unsigned short)rk[u];
-                        }
-                    }
-                }
-            }
-#else
             for (int k = 0; k < cnt; k++) {
                 const int t = trow + ta + k;
                 const int rk = atomicAdd(&hist[t], 1);
@@ -310,7 +287,6 @@ __global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__rest
                     }
                 }
             }
-#endif
         } else {
             for (int k = 0; k < cnt; k++) {
                 const int t = trow + ta + k;

@@ -83,12 +83,6 @@ struct StageT {                                   // PAD: list padding = entries
 constexpr int FWD_FU = 4;
 using StageFwd = StageT<1, FWD_FU>;
 constexpr int BWD_CHUNK = 64;
-#ifndef LGM_AB_LS
-#define LGM_AB_LS (BWD_CHUNK + 1)  // (A/B in progress) moment-slot row stride (71: the flush's (entry, partial) reads spread over the banks)
-#endif
-#ifndef LGM_AB_JUNK
-#define LGM_AB_JUNK 0  // (A/B in progress) 1: per-lane junk words for the dead moment-MFMA results
-#endif
 // backward lists are padded to MB with the sentinel: every list position is one MFMA batch column (k_render_bwd)
 using StageBwd = StageT<2, MB, BWD_CHUNK>;
 
@@ -691,7 +685,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     float *__restrict__ accum, const unsigned *__restrict__ det_max, unsigned *__restrict__ det_sat,
     long long item_stamps) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
-    constexpr int CH = BWD_CHUNK, LS = LGM_AB_LS;  // entries per staged chunk; padded LDS row stride
+    constexpr int CH = BWD_CHUNK, LS = CH + 1;  // entries per staged chunk; padded LDS row stride
     __shared__ StageBwd S;
     // per-wave moment slots (plain stores: each wave writes an entry's moments once; no LDS atomics), combined over
     // the entry's quadrant waves at the chunk's end (then they hold the entry's gradient partials, in wave 0's slot)
@@ -804,11 +798,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     for (int rr = 0; rr < 4; rr++) {
         const int row = 4 * qk + rr;
         const bool live = ql < MB ? row <= 5 : (row >= 6 && row < NROW);
-#if LGM_AB_JUNK
-        mrow[rr] = live ? row * LS : -1;  // (dead results go to this lane's own word of the junk row)
-#else
         mrow[rr] = live ? row * LS : NROW * LS;  // the junk row (all MB columns of a batch are stored)
-#endif
     }
     float *myAcc = sAccW[w];
     float *myWU = sWU[w];
@@ -893,13 +883,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         // D[row = 4 qk + r][col = ql]: moments 0..5 in the w columns, rows 6..9 in the u columns; each lane stores its
         // (at most 4) live results into this wave's slots at a per-lane row offset fixed for the kernel (mrow)
 #pragma unroll
-#if LGM_AB_JUNK
-        // (a dead result to the lane's own junk word: the shared junk row took up to 5 same-address writes per
-        // store instruction)
-        for (int rr = 0; rr < 4; rr++) myAcc[mrow[rr] >= 0 ? mrow[rr] + col : NROW * LS + lane] = acc[rr];
-#else
         for (int rr = 0; rr < 4; rr++) myAcc[mrow[rr] + col] = acc[rr];  // (sentinel columns: row CH, all zero)
-#endif
     };
 
     // Staging pipeline (front to back over [s0, s1)): chunk b0 + CH streams into the other buffer by LDS DMA

@@ -208,16 +208,12 @@ def step_spread(step, n: int) -> dict:
     in the line next to the timed mean."""
     import torch
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
-    import gc
-    gc.collect()
-    gc.disable()  # (as the timed loop: D.timed_steps)
     torch.cuda.synchronize()
     evs[0].record()
     for i in range(n):
         step()
         evs[i + 1].record()
     torch.cuda.synchronize()
-    gc.enable()
     d = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(n))
     return {"steps": n, "min_ms": round(d[0], 4), "median_ms": round(d[n // 2], 4), "max_ms": round(d[-1], 4)}
 

@@ -76,27 +76,17 @@ def max_over_ranks(x: float, info: RankInfo, device=None) -> float:
 def timed_steps(step: Callable[[], None], steps: int, info: RankInfo, sync: Callable[[], None],
                 device=None) -> float:
     """Time exactly `steps` calls of step(): barrier + sync on both sides, wall time maxed over ranks (seconds).
-    Python's cyclic garbage collector is paused for the timed region, as `timeit` does by default: a collector pass
-    stalls the launching thread, and one scene's step (~0.23 ms of GPU work, the host only ~0.06 ms ahead per
-    step) showed single 0.4-0.6 ms steps in bench.py's step spread. The step's tensors are still freed by reference
-    counting; nothing in the timed work changes."""
-    import gc
-    gc.collect()
-    was_enabled = gc.isenabled()
-    gc.disable()
-    try:
-        barrier(info)
-        sync()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-        sync()
-        barrier(info)
-        el = time.perf_counter() - t0
-    finally:
-        if was_enabled:
-            gc.enable()
-    return max_over_ranks(el, info, device)
+    (Python's collector stays on: paused for the timed region, the render step's autograd reference cycles kept
+    their 1.2 GB workspaces alive, the caching allocator had to map new blocks, and the single-scene step went
+    0.229 -> 0.243 ms median, profiles/r04/s3.)"""
+    barrier(info)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier(info)
+    return max_over_ranks(time.perf_counter() - t0, info, device)
 
 
 def _spawned_rank(local_rank, world, port, target, args):

@@ -76,9 +76,9 @@ def max_over_ranks(x: float, info: RankInfo, device=None) -> float:
 def timed_steps(step: Callable[[], None], steps: int, info: RankInfo, sync: Callable[[], None],
                 device=None) -> float:
     """Time exactly `steps` calls of step(): barrier + sync on both sides, wall time maxed over ranks (seconds).
-    (Python's collector stays on: paused for the timed region, the render step's autograd reference cycles kept
-    their 1.2 GB workspaces alive, the caching allocator had to map new blocks, and the single-scene step went
-    0.229 -> 0.243 ms median, profiles/r04/s3.)"""
+    (Python's collector stays on: paused for the timed region, the single-scene step went 0.229 -> 0.243 ms median
+    with unchanged kernel times, profiles/r04/s3_gc_paused -- presumably uncollected autograd reference cycles kept
+    step workspaces alive, so the caching allocator had to map new blocks.)"""
     barrier(info)
     sync()
     t0 = time.perf_counter()

@@ -787,8 +787,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                                                  const typename Ty<DT>::T *__restrict__ k,
                                                  const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                  const typename Ty<DT>::T *__restrict__ dout,
-                                                 const float *__restrict__ lse, const float *__restrict__ delta,
-                                                 typename Ty<DT>::T *__restrict__ dq, long long ldd) {
+                                                 const float *__restrict__ lse, float *__restrict__ delta,
+                                                 typename Ty<DT>::T *__restrict__ dq, long long ldd,
+                                                 const typename Ty<DT>::T *__restrict__ o) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
     constexpr int LDK = D + LDK_PAD;
@@ -809,7 +810,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         load_yfrag<DT, D>(qf[s], q + base + (long long)qr * ld, qv, g);
         load_yfrag<DT, D>(of[s], dout + obase + (long long)qr * H * D, qv, g);
         l2[s] = qv ? lse[(long long)bh * L + qr] * LOG2E : INFINITY;
-        dl[s] = qv ? delta[(long long)bh * L + qr] : 0.f;
+        // delta = rowsum(dO o O) of this lane's row, here instead of a separate pass: each of the row's four lanes
+        // (g) holds D / 4 of its elements; their partial sums meet by two lane exchanges, and lane g = 0 stores the
+        // row's delta for k_attn_dkdv2 (launched after this kernel)
+        {
+            YFrag<DT, D> ofr;
+            load_yfrag<DT, D>(ofr, o + obase + (long long)qr * H * D, qv, g);
+            float part = 0.f;
+#pragma unroll
+            for (int cc = 0; cc < D / 32; cc++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) part = fmaf((float)ofr.v[cc][j], (float)of[s].v[cc][j], part);
+            part += __shfl_xor(part, 16, 64);
+            part += __shfl_xor(part, 32, 64);
+            dl[s] = qv ? part : 0.f;
+            if (qv && g == 0) delta[(long long)bh * L + qr] = part;
+        }
         prescale<DT, D / 32>(qf[s].v, c);  // S in log2 units
     }
     f32x4 dqa[QS][D / 16];
@@ -925,25 +941,25 @@ int bwd_impl(int B, int L, int H, float scale, const void *q, const void *k, con
              float *delta, hipStream_t st) {
     using T = typename Ty<DT>::T;
     const long long rows = (long long)B * L * H;
-    LGM_LAUNCH("k_attn_delta", st, (k_attn_delta<DT, D><<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(
-                                       B, L, H, (const T *)o, (const T *)dout, delta)));
-    if constexpr (DT != LGM_ATTN_F32) {
+    if constexpr (DT != LGM_ATTN_F32) {  // (delta computed by k_attn_dq2 itself)
         constexpr int S2 = D <= 32 ? 2 : 1;  // two 16-row sub-tiles per wavefront where registers allow
         const bool two = S2 == 2 && (long long)((L + 127) / 128) * B * H >= 512;
         dim3 g2((L + (two ? 127 : 63)) / (two ? 128 : 64), B * H);
         if (two) {
             LGM_LAUNCH("k_attn_dq", st, (k_attn_dq2<DT, D, S2><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
-                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd)));
+                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd, (const T *)o)));
             LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, S2><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
                        (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dk, (T *)dv, ldd)));
         } else {
             LGM_LAUNCH("k_attn_dq", st, (k_attn_dq2<DT, D, 1><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
-                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd)));
+                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd, (const T *)o)));
             LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, 1><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
                        (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dk, (T *)dv, ldd)));
         }
         return LGM_OK;
     }
+    LGM_LAUNCH("k_attn_delta", st, (k_attn_delta<DT, D><<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(
+                                       B, L, H, (const T *)o, (const T *)dout, delta)));
     dim3 grid((L + 63) / 64, B * H);
     LGM_LAUNCH("k_attn_dq", st, (k_attn_dq<DT, D><<<grid, NT, 0, st>>>(L, H, scale, (const T *)q, (const T *)k,
                                                                      (const T *)v, ld, (const T *)dout, lse, delta,

@@ -44,6 +44,4 @@ def test_ply_bytes_follow_the_reference_recipe(tmp_path):
     want = header.encode("ascii") + el.astype(el.dtype.newbyteorder("<")).tobytes()
     got = open(p, "rb").read()
     assert got[:len(header)] == want[:len(header)]
-    body_got = np.frombuffer(got[len(header):], dtype="<f4").reshape(-1, 14)
-    body_want = np.frombuffer(want[len(header):], dtype="<f4").reshape(-1, 14)
-    np.testing.assert_allclose(body_got, body_want, rtol=1e-6, atol=1e-7)
+    assert got == want  # byte for byte, body included

@@ -76,12 +76,9 @@ def max_over_ranks(x: float, info: RankInfo, device=None) -> float:
 def timed_steps(step: Callable[[], None], steps: int, info: RankInfo, sync: Callable[[], None],
                 device=None) -> float:
     """Time exactly `steps` calls of step(): barrier + sync on both sides, wall time maxed over ranks (seconds).
-    Python's collector stays on, but a full collection runs first, outside the timed region: the step allocates
-    enough container objects for a generation-1 collection (~0.3 ms in the bench process) every ~70 steps, so a
-    40-step loop otherwise caught one about every other run (+7.5 us per single-scene step, profiles/r04/diag_host:
-    host launch work 130 us vs 225 us of GPU work per step, so the loop is GPU-bound between collections)."""
-    import gc
-    gc.collect()
+    Python's collector is left as it is: a full collection right before the loop made the next few dozen single-scene
+    steps ~16 us slower on the GPU (profiles/r04/diag_host: 225 -> 241 us per step, host work unchanged), and pausing
+    it for the loop measured slower too (profiles/r04/s3_gc_paused)."""
     barrier(info)
     sync()
     t0 = time.perf_counter()

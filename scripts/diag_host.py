@@ -1,7 +1,9 @@
 """Host overhead of bench.py's single-scene (cfg3) step: per-step host time (the Python / autograd / C-ABI launch
 work, no sync) next to the GPU's per-step time (events between steps), the garbage collections that ran inside
 the loop, and the timed mean -- to tell whether the timed loop is host-starved.
-Usage: python scripts/diag_host.py [--steps 200] [--gc off|on|freeze]"""
+--pool-first runs bench.py's 8-scene pool steps first (as bench.py does before its cfg3 loop) and --warmup sets
+the single-scene warmup; the per-step (host, GPU) times of the first 12 timed steps are printed too.
+Usage: python scripts/diag_host.py [--steps 200] [--warmup 20] [--gc off|on|freeze|collect] [--pool-first]"""
 import argparse
 import gc
 import json
@@ -16,10 +18,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--gc", default="on", choices=["on", "off", "freeze"])
+    ap.add_argument("--gc", default="on", choices=["on", "off", "freeze", "collect"])
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--pool-first", action="store_true")
     a = ap.parse_args()
     import torch
-    from bench import CFG3_SEED, N_GAUSS, RES, VIEWS
+    from bench import CFG3_SEED, N_GAUSS, POOL_SCENES, POOL_SEED, RES, VIEWS
     from lgm_amd import GaussianRenderer, Options
     from lgm_amd.cameras import orbit_cameras
     from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads
@@ -37,7 +41,19 @@ def main():
         torch.autograd.backward([out["image"], out["alpha"]], [d3i, d3a])
         g3.grad = None
 
-    for _ in range(20):
+    if a.pool_first:
+        gp = synthetic_gaussians(POOL_SCENES, N_GAUSS, seed=POOL_SEED).to(dev).requires_grad_(True)
+        dpi, _, dpa, bgp = synthetic_upstream_grads(POOL_SCENES, VIEWS, RES, RES, seed=POOL_SEED + 1000)
+        B = POOL_SCENES
+        cvb, cvpb = (x[None].expand(B, -1, -1, -1).contiguous().to(dev) for x in (cv, cvp))
+        cpb = cp[None].expand(B, -1, -1).contiguous().to(dev)
+        dpi, dpa, bgp = dpi.to(dev), dpa.to(dev), bgp.to(dev)
+        for _ in range(40):
+            out = r.render(gp, cvb, cvpb, cpb, bg_color=bgp)
+            torch.autograd.backward([out["image"], out["alpha"]], [dpi, dpa])
+            gp.grad = None
+        del out
+    for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
     gcs = []
@@ -51,6 +67,8 @@ def main():
     gc.callbacks.append(cb)
     if a.gc == "off":
         gc.disable()
+    elif a.gc == "collect":
+        gc.collect()
     elif a.gc == "freeze":
         gc.collect()
         gc.freeze()
@@ -78,6 +96,7 @@ def main():
     print(json.dumps({"gc": a.gc, "steps": n, "timed_mean_us": round(1e6 * el / n, 1), "host_us": st(host),
                       "gpu_us": st(gpu), "gc_runs": len(gcs),
                       "gc_us_by_gen": {gen: round(sum(t for g, t in gcs if g == gen), 1) for gen in (0, 1, 2)},
+                      "first12": [(round(host[i], 1), round(gpu[i], 1)) for i in range(min(12, n))],
                       "slow_steps": [(i, round(host[i], 1), round(gpu[i], 1)) for i in range(n) if gpu[i] > 260][:20]}))
 
 

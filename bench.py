@@ -233,6 +233,7 @@ def attention_bench(dev, steps: int = 10):
     import torch.nn.functional as F
 
     from lgm_amd import _native
+    from lgm_amd import dist as Dist
     from lgm_amd.attention import packed_attention
     B, L, H, D = 8, 4096, 16, 32
     g = torch.Generator(device="cpu").manual_seed(7)
@@ -245,8 +246,7 @@ def attention_bench(dev, steps: int = 10):
         packed_attention(x).backward(d_o)
 
     def timed(fn):
-        fn()
-        torch.cuda.synchronize()
+        Dist.warm_up(fn, 1, torch.cuda.synchronize)
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record()
         for _ in range(steps):
@@ -299,10 +299,9 @@ def cfg2_bench(dev, steps):
     g = synthetic_gaussians(1, 50_000, seed=CFG2_SEED).to(dev)
     cv, cvp, cp = (t[None].to(dev) for t in orbit_cameras(1))
     bg = torch.ones(3, device=dev)
+    from lgm_amd import dist as D
     with torch.no_grad():
-        for _ in range(5):
-            r.render(g, cv, cvp, cp, bg_color=bg)
-        torch.cuda.synchronize()
+        D.warm_up(lambda: r.render(g, cv, cvp, cp, bg_color=bg), 5, torch.cuda.synchronize)
         t0 = time.perf_counter()
         for _ in range(steps):
             r.render(g, cv, cvp, cp, bg_color=bg)
@@ -328,6 +327,7 @@ def cfg4_bench(dev, steps):
     import torch
 
     from lgm_amd import GaussianRenderer, Options
+    from lgm_amd import dist as D
     from lgm_amd.attention import MVAttention
     from lgm_amd.cameras import orbit_cameras
     from lgm_amd.synthetic import synthetic_gaussians
@@ -354,9 +354,7 @@ def cfg4_bench(dev, steps):
             r.render(g, cv, cvp, cp, bg_color=bg)
 
     def timed(fn):
-        for _ in range(2):
-            fn()
-        torch.cuda.synchronize()
+        D.warm_up(fn, 2, torch.cuda.synchronize)
         t0 = time.perf_counter()
         for _ in range(steps):
             fn()
@@ -424,8 +422,7 @@ def cfg5_bench(dev, info, steps):
         head.zero_grad()
 
     def timed(fn, n):
-        for _ in range(2):
-            fn()
+        D.warm_up(fn, 2, torch.cuda.synchronize, info, dev)
         return 1e3 * D.timed_steps(fn, n, info, torch.cuda.synchronize, dev) / n
 
     res = {"workload": "cfg5 render side (main.py:82-109, one object per GPU): Gaussian head (6 x 160^2 -> "
@@ -488,8 +485,7 @@ def run(args):
         torch.autograd.backward([out["image"], out["alpha"]], [d_imgd, d_alphad])
         g.grad = None
 
-    for _ in range(args.warmup):
-        step()
+    D.warm_up(step, args.warmup, torch.cuda.synchronize, info, dev)  # (>= 50 ms: the clocks' ramp, dist.warm_up)
     # timed steps with nothing attached; per-kernel HIP-event times from a second, untimed pass of the same steps
     el = D.timed_steps(step, args.steps, info, torch.cuda.synchronize, dev)
     prof = _native.KernelProfiler()
@@ -507,8 +503,7 @@ def run(args):
     if not args.no_det and not args.only_pool:  # (PMC runs: only the headline kernels, float atomics)
         os.environ["LGM_AMD_DETERMINISTIC"] = "1"
         try:
-            for _ in range(max(2, args.warmup // 2)):
-                step()
+            D.warm_up(step, max(2, args.warmup // 2), torch.cuda.synchronize, info, dev)
             n_det = max(5, args.steps // 2)
             el_det = D.timed_steps(step, n_det, info, torch.cuda.synchronize, dev)
             prof_d = _native.KernelProfiler()
@@ -603,8 +598,7 @@ def run(args):
         D.allreduce_scene_grads(grad, info)
         g3.grad = None
 
-    for _ in range(args.warmup):
-        step3()
+    D.warm_up(step3, args.warmup, torch.cuda.synchronize, info, dev)
     el3 = D.timed_steps(step3, args.steps, info, torch.cuda.synchronize, dev)
     prof3 = _native.KernelProfiler()  # per-kernel times of the single-scene step (a separate, untimed pass)
     with prof3:

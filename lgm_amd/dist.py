@@ -73,6 +73,31 @@ def max_over_ranks(x: float, info: RankInfo, device=None) -> float:
     return float(t.item())
 
 
+def warm_up(step: Callable[[], None], steps: int, sync: Callable[[], None], info: RankInfo = None, device=None,
+            min_seconds: float = 0.05) -> int:
+    """Untimed warmup: `steps` calls of step() (at least one), then as many more as bring the warmup to min_seconds of
+    wall time at the measured rate -- the same count on every rank (max over ranks), so steps that hold collectives
+    stay matched. Returns the number of calls. The GPU's clocks ramp under load: a single-scene step takes ~240 us
+    for its first ~60 steps after a pause (253 us after 100 ms idle) and 224-225 us from ~15-20 ms of continuous
+    work on (profiles/r04/diag_idle), so a warmup counted only in steps (10 x 0.23 ms) left the whole timed loop on
+    the ramp."""
+    import math
+    import time
+    steps = max(1, steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    el = time.perf_counter() - t0
+    extra = math.ceil(max(0.0, min_seconds - el) / (el / steps)) if el > 0 else 0
+    if info is not None and info.world > 1:
+        extra = int(max_over_ranks(float(extra), info, device))
+    for _ in range(extra):
+        step()
+    sync()
+    return steps + extra
+
+
 def timed_steps(step: Callable[[], None], steps: int, info: RankInfo, sync: Callable[[], None],
                 device=None) -> float:
     """Time exactly `steps` calls of step(): barrier + sync on both sides, wall time maxed over ranks (seconds).

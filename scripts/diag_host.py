@@ -3,7 +3,9 @@ work, no sync) next to the GPU's per-step time (events between steps), the garba
 the loop, and the timed mean -- to tell whether the timed loop is host-starved.
 --pool-first runs bench.py's 8-scene pool steps first (as bench.py does before its cfg3 loop) and --warmup sets
 the single-scene warmup; the per-step (host, GPU) times of the first 12 timed steps are printed too.
-Usage: python scripts/diag_host.py [--steps 200] [--warmup 20] [--gc off|on|freeze|collect] [--pool-first]"""
+--idle-ms sleeps (GPU idle) before the loop; gpu_us_by_20 = mean GPU time per step over each 20 steps.
+Usage: python scripts/diag_host.py [--steps 200] [--warmup 20] [--gc off|on|freeze|collect] [--pool-first]
+       [--idle-ms MS]"""
 import argparse
 import gc
 import json
@@ -21,6 +23,7 @@ def main():
     ap.add_argument("--gc", default="on", choices=["on", "off", "freeze", "collect"])
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--pool-first", action="store_true")
+    ap.add_argument("--idle-ms", type=float, default=0.0, help="sleep this long (GPU idle) before the timed loop")
     a = ap.parse_args()
     import torch
     from bench import CFG3_SEED, N_GAUSS, POOL_SCENES, POOL_SEED, RES, VIEWS
@@ -73,6 +76,9 @@ def main():
         gc.collect()
         gc.freeze()
     n = a.steps
+    if a.idle_ms > 0:
+        torch.cuda.synchronize()
+        time.sleep(a.idle_ms / 1e3)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
     host = []
     torch.cuda.synchronize()
@@ -96,6 +102,8 @@ def main():
     print(json.dumps({"gc": a.gc, "steps": n, "timed_mean_us": round(1e6 * el / n, 1), "host_us": st(host),
                       "gpu_us": st(gpu), "gc_runs": len(gcs),
                       "gc_us_by_gen": {gen: round(sum(t for g, t in gcs if g == gen), 1) for gen in (0, 1, 2)},
+                      "idle_ms": a.idle_ms,
+                      "gpu_us_by_20": [round(statistics.fmean(gpu[i:i + 20]), 1) for i in range(0, n, 20)],
                       "first12": [(round(host[i], 1), round(gpu[i], 1)) for i in range(min(12, n))],
                       "slow_steps": [(i, round(host[i], 1), round(gpu[i], 1)) for i in range(n) if gpu[i] > 260][:20]}))
 

@@ -72,6 +72,18 @@ def _worker(rank, port, tmp, mode):
 
             el = D.timed_steps(step, 3, info, sync=lambda: None)
             np.savez(os.path.join(tmp, f"r{rank}.npz"), el=np.array(el), calls=np.array(len(calls)))
+        elif mode == "warmup":
+            import time
+            import torch.distributed as dist
+            dt = 0.004 * (1 + 3 * rank)  # rank 1 is 4x slower: alone it would need fewer calls for the same time
+
+            def step():
+                time.sleep(dt)
+                t = torch.ones(1)
+                dist.all_reduce(t)  # a collective inside the step: the ranks' call counts must match
+
+            n = D.warm_up(step, 2, sync=lambda: None, info=info, min_seconds=0.1)
+            np.savez(os.path.join(tmp, f"r{rank}.npz"), n=np.array(n))
     finally:
         D.finalize(info)
 
@@ -232,3 +244,12 @@ def test_timed_steps_max_over_ranks(tmp_path):
     assert els[0] == els[1]  # every rank reports the max
     assert els[0] >= 3 * 0.1 * 0.95  # the slow rank's 3 x 0.1 s
     assert all(int(r["calls"]) == 3 for r in res)
+
+
+def test_warm_up_matches_call_counts_over_ranks(tmp_path):
+    """dist.warm_up tops the W warmup steps up to a minimum wall time (the GPU clocks' ramp) with the same number of
+    calls on every rank, so a step holding a collective cannot deadlock."""
+    res = _run("warmup", tmp_path)
+    ns = [int(r["n"]) for r in res]
+    assert ns[0] == ns[1] and ns[0] >= 2
+    assert ns[0] * 0.016 >= 0.1 * 0.8  # the collective paces both ranks at the slow one's 16 ms per step

@@ -16,6 +16,7 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from lgm_amd import _native  # noqa: E402
+from lgm_amd.dist import warm_up  # noqa: E402
 from lgm_amd.attention import packed_attention  # noqa: E402
 
 # (name, B objects, views F, tokens per view h*w, heads, head dim)
@@ -30,8 +31,7 @@ LEVELS = [
 
 def timed(fn, iters):
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fn()
-    torch.cuda.synchronize()
+    warm_up(fn, 1, torch.cuda.synchronize)  # >= 50 ms: the GPU clocks' ramp (lgm_amd/dist.py)
     st.record()
     for _ in range(iters):
         fn()

@@ -695,7 +695,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     };
     auto store_rows2 = [&](int buf) {
         ld_.store(Qs[buf], Os[buf], LDK);
-        if (tid < 64) { sl[buf][tid] = -pl; sd[buf][tid] = -pd; }  // stored negated: the accumulator inits
+        if (tid < 64) {  // stored negated: the accumulator inits
+            // (the row index recomputed here: the two LDS addresses hoisted out of the query loop were spilled at the
+            // 128-VGPR cap, and their scratch reloads sat on wave 0's path to every tile's barrier)
+            int row = tid;
+            asm volatile("" : "+v"(row));
+            sl[buf][row] = -pl;
+            sd[buf][row] = -pd;
+        }
     };
     load_rows2(0);
     store_rows2(0);

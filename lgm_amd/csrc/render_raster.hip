@@ -54,6 +54,10 @@ __device__ __forceinline__ int wave_max_i32(int v) {
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 constexpr int WU_LD = 68;  // row stride of the per-wave [16 columns][64 pixels] gradient image (16-B aligned rows)
+// Columns 4..11 of that image hold pixel p at p ^ 8 (WU_SWZ): with the 17-slot row stride this puts the 16 lanes of
+// every ds_read_b128 group of the batch reads (lanes {0-3, 12-15, 20-27}, ... : MI355X_MICROARCH.md §LDS) on 16
+// distinct 16-B slots; unswizzled, columns 10, 11 and 12, 13 of one group shared two slots (2-way).
+__device__ __forceinline__ int wu_swz(int col) { return (col >= 4 && col < 12) ? 8 : 0; }
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
 typedef __attribute__((ext_vector_type(2))) float f32x2v;
@@ -685,16 +689,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     float *__restrict__ accum, const unsigned *__restrict__ det_max, unsigned *__restrict__ det_sat,
     long long item_stamps) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
-    constexpr int CH = BWD_CHUNK, LS = CH + 1;  // entries per staged chunk; padded LDS row stride
+    // entries per staged chunk; LDS row stride of the moment slots: LS = 4 (mod 32) puts the rows a moment store
+    // writes at once (4 qk + rr, qk = 0, 1 in a 32-lane store group: rows rr and rr + 4) 16 banks apart, so a batch's
+    // 8 consecutive entry columns land on distinct banks (ds_write_b32 banks are (a / 4) mod 32)
+    constexpr int CH = BWD_CHUNK, LS = CH + 4;
     __shared__ StageBwd S;
     // per-wave moment slots (plain stores: each wave writes an entry's moments once; no LDS atomics), combined over
     // the entry's quadrant waves at the chunk's end (then they hold the entry's gradient partials, in wave 0's slot)
-    // (row NV of each wave's slot is a junk row: the MFMA results a lane does not keep are stored there, so the
-    // stores need no exec-masked branches)
     // moment rows: 0..5 geometric (w columns), then dL/dpixel-hi and dL/dpixel-lo sums of the NC colour [+ depth]
-    // channels (u columns); row NROW is the junk row
+    // channels (u columns). The MFMA results a lane does not keep go to a junk area after the rows (JB), each lane
+    // class of a store to its own 8-bank range there (mrow below), so the stores need no exec-masked branches and
+    // put no two lanes of a 32-lane group on one bank while the batch's columns are consecutive
     constexpr int NC = DEPTH ? 4 : 3, NROW = 6 + 2 * NC;
-    constexpr int SLOT = (LS * (NROW + 1) + 3) & ~3;  // 16-B aligned slots (zeroed by float4)
+    constexpr int JB = (LS * NROW + 31) & ~31, SLOT = JB + 32 + CH + 4;  // 16-B aligned slots
+    constexpr int ZSLOT = (LS * NROW + 3) & ~3;  // the part zeroed per chunk (the junk area is never read)
     __shared__ __attribute__((aligned(16))) float sAccW[4][SLOT];
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
     static_assert((NV + 3) * LS <= 16 * WU_LD, "the partial rows fit wave 0's WU image");
@@ -793,15 +801,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const float cxT = (float)tx0 + 7.5f, cyT = (float)ty0 + 7.5f;
     // the slot row offset of this lane's result r (row 4 qk + r of column ql), -1 where that result is unused:
     // w columns keep the geometric moments (rows 0..5), u columns the colour / depth sums (rows 6..8 [9])
+    // Banks: with LS = 4 (mod 32) the four lane classes of a 32-lane store group -- (qk, w or u column) for the
+    // group's two qk -- sit at rr LS + 8 m (mod 32), m = 0..3: a live row 4 qk + rr at m = 2 (qk & 1), the dead
+    // classes on the free m, so the group's 32 lanes cover the 32 banks once (8 consecutive columns per class).
     int mrow[4];
+    static_assert(LS % 32 == 4, "moment-slot bank layout");
 #pragma unroll
     for (int rr = 0; rr < 4; rr++) {
+        auto is_live = [&](int qq, bool ucol) {
+            const int row = 4 * qq + rr;
+            return ucol ? (row >= 6 && row < NROW) : row <= 5;
+        };
+        const bool ucol = ql >= MB;
         const int row = 4 * qk + rr;
-        const bool live = ql < MB ? row <= 5 : (row >= 6 && row < NROW);
-        mrow[rr] = live ? row * LS : NROW * LS;  // the junk row (all MB columns of a batch are stored)
+        const bool live = is_live(qk, ucol);
+        const int m = 2 * (qk & 1) + (live ? 0 : (is_live(qk, !ucol) || ucol ? 1 : 0));
+        mrow[rr] = live ? row * LS : JB + ((rr * LS + 8 * m) & 31);
     }
     float *myAcc = sAccW[w];
     float *myWU = sWU[w];
+    const int lane_x = lane ^ 8;  // this lane's pixel in the swizzled image columns (wu_swz)
     myWU[lane] = dp0;
     myWU[64 + lane] = dp1;
     myWU[128 + lane] = dp2;
@@ -848,8 +867,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     auto read_batch = [&](float (&xs)[2][8]) {
 #pragma unroll
         for (int t2 = 0; t2 < 2; t2++) {
-            const float4 *src = reinterpret_cast<const float4 *>(myWU + ql * WU_LD + 32 * t2 + 8 * qk);
-            const float4 x0 = src[0], x1 = src[1];
+            const float *row = myWU + ql * WU_LD;
+            const int p0 = 32 * t2 + 8 * qk, sw = wu_swz(ql);
+            const float4 x0 = *reinterpret_cast<const float4 *>(row + (p0 ^ sw));
+            const float4 x1 = *reinterpret_cast<const float4 *>(row + ((p0 + 4) ^ sw));
             xs[t2][0] = x0.x; xs[t2][1] = x0.y; xs[t2][2] = x0.z; xs[t2][3] = x0.w;
             xs[t2][4] = x1.x; xs[t2][5] = x1.y; xs[t2][6] = x1.z; xs[t2][7] = x1.w;
         }
@@ -910,7 +931,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
            // entries loop follows the quadrant tests without a barrier (with the conversion over three waves below:
            // pool k_render_bwd 642 -> 635 us, bitwise equal, profiles/r04/ab_bwd_conv)
             float4 *z = reinterpret_cast<float4 *>(myAcc);
-            for (int q = lane; q < SLOT / 4; q += 64) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q = lane; q < ZSLOT / 4; q += 64) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         int cnt;
         {
@@ -984,8 +1005,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                     Erem = fmaf(-aT, cdp, Erem);
                     const float dL_dalpha = fmaf(Tr, cdp, -Erem * inv);
                     Tr = Tr - aT;
-                    myWU[(4 * h + u) * WU_LD + lane] = Gw[u] * dL_dalpha;  // w
-                    myWU[(MB + 4 * h + u) * WU_LD + lane] = aT;            // u (dchannel_dcolor)
+                    // w (columns 0..7) and u (8..15), pixel lane at lane ^ wu_swz(column): the swizzled
+                    // columns 4..7 and 8..11 are h = 1 for w, h = 0 for u
+                    myWU[(4 * h + u) * WU_LD + (h == 1 ? lane_x : lane)] = Gw[u] * dL_dalpha;
+                    myWU[(MB + 4 * h + u) * WU_LD + (h == 0 ? lane_x : lane)] = aT;  // (dchannel_dcolor)
                 }
             }
         };

@@ -692,7 +692,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // entries per staged chunk; LDS row stride of the moment slots: LS = 4 (mod 32) puts the rows a moment store
     // writes at once (4 qk + rr, qk = 0, 1 in a 32-lane store group: rows rr and rr + 4) 16 banks apart, so a batch's
     // 8 consecutive entry columns land on distinct banks (ds_write_b32 banks are (a / 4) mod 32)
-    constexpr int CH = BWD_CHUNK, LS = CH + 4;
+    // (the depth-gradient instantiation keeps stride 65 and one shared junk row: its larger slots would not leave
+    // room for a fourth workgroup per CU otherwise)
+    constexpr int CH = BWD_CHUNK, LS = DEPTH ? CH + 1 : CH + 4;
     __shared__ StageBwd S;
     // per-wave moment slots (plain stores: each wave writes an entry's moments once; no LDS atomics), combined over
     // the entry's quadrant waves at the chunk's end (then they hold the entry's gradient partials, in wave 0's slot)
@@ -701,7 +703,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // class of a store to its own 8-bank range there (mrow below), so the stores need no exec-masked branches and
     // put no two lanes of a 32-lane group on one bank while the batch's columns are consecutive
     constexpr int NC = DEPTH ? 4 : 3, NROW = 6 + 2 * NC;
-    constexpr int JB = (LS * NROW + 31) & ~31, SLOT = JB + 32 + CH + 4;  // 16-B aligned slots
+    constexpr int JB = DEPTH ? LS * NROW : (LS * NROW + 31) & ~31;
+    constexpr int SLOT = DEPTH ? (LS * (NROW + 1) + 3) & ~3 : JB + 32 + CH + 4;  // 16-B aligned slots
     constexpr int ZSLOT = (LS * NROW + 3) & ~3;  // the part zeroed per chunk (the junk area is never read)
     __shared__ __attribute__((aligned(16))) float sAccW[4][SLOT];
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
@@ -805,7 +808,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // group's two qk -- sit at rr LS + 8 m (mod 32), m = 0..3: a live row 4 qk + rr at m = 2 (qk & 1), the dead
     // classes on the free m, so the group's 32 lanes cover the 32 banks once (8 consecutive columns per class).
     int mrow[4];
-    static_assert(LS % 32 == 4, "moment-slot bank layout");
+    static_assert(DEPTH || LS % 32 == 4, "moment-slot bank layout");
 #pragma unroll
     for (int rr = 0; rr < 4; rr++) {
         auto is_live = [&](int qq, bool ucol) {
@@ -816,7 +819,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         const int row = 4 * qk + rr;
         const bool live = is_live(qk, ucol);
         const int m = 2 * (qk & 1) + (live ? 0 : (is_live(qk, !ucol) || ucol ? 1 : 0));
-        mrow[rr] = live ? row * LS : JB + ((rr * LS + 8 * m) & 31);
+        mrow[rr] = live ? row * LS : DEPTH ? JB : JB + ((rr * LS + 8 * m) & 31);
     }
     float *myAcc = sAccW[w];
     float *myWU = sWU[w];

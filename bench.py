@@ -487,7 +487,8 @@ def run(args):
 
     D.warm_up(step, args.warmup, torch.cuda.synchronize, info, dev)  # (>= 50 ms: the clocks' ramp, dist.warm_up)
     # timed steps with nothing attached; per-kernel HIP-event times from a second, untimed pass of the same steps
-    el = D.timed_steps(step, args.steps, info, torch.cuda.synchronize, dev)
+    stamps = {}
+    el = D.timed_steps(step, args.steps, info, torch.cuda.synchronize, dev, stamps=stamps)
     prof = _native.KernelProfiler()
     with prof:
         for _ in range(args.steps):
@@ -546,6 +547,7 @@ def run(args):
                    "pairs_binned_rank0": K_binned, "parallelism": f"scene-sharded x{world} (no collective)"},
         "kernels": per_kernel,
         "step_spread": spread,
+        "timed_loop": stamps,
         "profiled_kernel_sum_ms_per_step": kernel_sum_ms(kern, args.steps),
     }
     if det:
@@ -599,7 +601,8 @@ def run(args):
         g3.grad = None
 
     D.warm_up(step3, args.warmup, torch.cuda.synchronize, info, dev)
-    el3 = D.timed_steps(step3, args.steps, info, torch.cuda.synchronize, dev)
+    stamps3 = {}
+    el3 = D.timed_steps(step3, args.steps, info, torch.cuda.synchronize, dev, stamps=stamps3)
     prof3 = _native.KernelProfiler()  # per-kernel times of the single-scene step (a separate, untimed pass)
     with prof3:
         for _ in range(args.steps):
@@ -620,7 +623,7 @@ def run(args):
         "ms_per_step": round(1e3 * el3 / args.steps, 4),
         "Mpixels_per_s": round(VIEWS * P * args.steps / el3 / 1e6, 2),
         "allreduce_ms": round(ar["ms"], 4) if world > 1 else None,
-        "step_spread": spread3, "profiled_kernel_sum_ms_per_step": kernel_sum_ms(kern3, args.steps),
+        "step_spread": spread3, "timed_loop": stamps3, "profiled_kernel_sum_ms_per_step": kernel_sum_ms(kern3, args.steps),
         "kernels": {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in kern3.items()}}
 
     if not args.no_cfg5:  # every rank (its all-reduce is collective)

@@ -25,7 +25,8 @@ extern "C" {
 /* Thread-local description of the last error ("" if none). */
 const char *lgm_last_error(void);
 
-/* ABI version (bumped on any signature change). 3: per-call lgm_diag, LGM_RENDER_NO_CULL as a per-call option. */
+/* ABI version (bumped on any signature change). 3: per-call lgm_diag, LGM_RENDER_NO_CULL as a per-call option.
+ * 4: lgm_diag.det_limit_log2. */
 int lgm_abi_version(void);
 
 /* Profiler object: create, read per-kernel totals, reset, destroy. It records into itself only while a call is
@@ -41,6 +42,9 @@ void lgm_profiler_destroy(lgm_profiler *p);
 typedef struct lgm_diag {
     lgm_profiler *profiler;              /* HIP events around every kernel of the call, or NULL */
     unsigned long long *render_counters; /* DEVICE work counters of the render kernels (see lgm_render.h), or NULL */
+    int det_limit_log2;                  /* test hook, 0 = none: LGM_RENDER_DETERMINISTIC's per-flush overflow bound
+                                            becomes 2^det_limit_log2 instead of 2^62 / 2^ceil(log2 tiles), so a test
+                                            can force the saturation path (gradients poisoned with NaN) */
 } lgm_diag;
 
 #ifdef __cplusplus

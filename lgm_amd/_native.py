@@ -66,7 +66,7 @@ SIGNATURES = {
 _lib = None
 
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 RENDER_NO_CULL = 1  # include/lgm_render.h LGM_RENDER_NO_CULL
 RENDER_CLAMP_IMAGE = 2  # include/lgm_render.h LGM_RENDER_CLAMP_IMAGE
 RENDER_BACKWARD_AGAIN = 4  # include/lgm_render.h LGM_RENDER_BACKWARD_AGAIN
@@ -117,7 +117,7 @@ def require_device_tensor(t: torch.Tensor, name: str):
 
 class _Diag(ctypes.Structure):
     """include/lgm_common.h lgm_diag."""
-    _fields_ = [("profiler", _vp), ("render_counters", _vp)]
+    _fields_ = [("profiler", _vp), ("render_counters", _vp), ("det_limit_log2", ctypes.c_int)]
 
 
 _diag_cur = None  # the lgm_diag every wrapper passes while a diagnostics() block is open (None: NULL)
@@ -130,13 +130,14 @@ def diag():
 
 
 @contextlib.contextmanager
-def diagnostics(profiler=None, render_counters=None):
+def diagnostics(profiler=None, render_counters=None, det_limit_log2=0):
     """Inside the block, every liblgm_amd call made through this package carries these diagnostics: a
-    KernelProfiler and/or a device uint64 tensor for the render work counters (include/lgm_render.h)."""
+    KernelProfiler and/or a device uint64 tensor for the render work counters (include/lgm_render.h), and the
+    deterministic mode's overflow-bound test hook (include/lgm_common.h)."""
     global _diag_cur
     prev = _diag_cur
     d = _Diag(profiler.h if profiler is not None else None,
-              render_counters.data_ptr() if render_counters is not None else None)
+              render_counters.data_ptr() if render_counters is not None else None, int(det_limit_log2))
     _diag_cur = d
     try:
         yield d

@@ -33,6 +33,7 @@ int check_common(int B, int V, int N, int H, int W, const void *g, const void *c
     d.mod = mod;
     const lgm_diag *diag = lgm::call_diag();  // this call's diagnostics (DiagScope), or none
     d.counters = diag ? diag->render_counters : nullptr;
+    d.det_lim_log2 = diag ? diag->det_limit_log2 : 0;
     d.options = 0;
     d.gt_img = d.gt_mask = nullptr;
     d.loss_part = d.loss_out = nullptr;

@@ -103,6 +103,7 @@ struct Dims {
     int B, V, N, H, W, gx, gy, T, BV;
     float tanx, tany, fx, fy, mod;
     unsigned long long *counters;  // this call's device work counters (lgm_diag.render_counters), or null
+    int det_lim_log2;              // lgm_diag.det_limit_log2 (test hook; 0 = the derived bound)
     int options;                   // per-call LGM_RENDER_* bits (NO_CULL, CLAMP_IMAGE, FUSED_LOSS, DETERMINISTIC)
     // LGM_RENDER_FUSED_LOSS (core/models.py:138-160): ground truth [BV,3,P] / [BV,P], the per-tile loss partials
     // (forward) and the gradients of the two MSE terms (backward)

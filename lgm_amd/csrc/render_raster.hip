@@ -627,8 +627,11 @@ __global__ __launch_bounds__(256) void k_det_seed_max(Dims d, const float *__res
                                                       const float *__restrict__ d_img, const float *__restrict__ d_depth,
                                                       const float *__restrict__ d_alpha,
                                                       const unsigned char *__restrict__ cmask,
-                                                      unsigned *__restrict__ det_max) {
+                                                      unsigned *__restrict__ det_max, unsigned *__restrict__ det_sat) {
     __shared__ unsigned s_m[4];
+    // the call's overflow count starts at zero here, ahead of every k_render_bwd flush of the call (a repeated
+    // backward of the same forward, LGM_RENDER_BACKWARD_AGAIN, must not inherit an earlier backward's count)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *det_sat = 0u;
     int lx, ly;
     tile_pixel(threadIdx.x, lx, ly);
     const size_t P = (size_t)d.H * d.W;
@@ -798,6 +801,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     float Erem = DK - Dup;  // Dfin - K - D_i, kept directly (one subtraction less per entry)
     const float ddelx_dx = 0.5f * d.W, ddely_dy = 0.5f * d.H;
     const int det_s = DET ? det_seed_shift(det_max) : 0;
+    const float det_lim = ldexpf(1.f, d.det_lim_log2 ? d.det_lim_log2  // (2^62 / 2^ceil(log2 T))
+                                                     : 62 - (d.T > 1 ? 32 - __clz(d.T - 1) : 0));
     const size_t gbase = (size_t)bv * d.N;
     // MFMA operands: A (features) lane (ql, qk) holds feature ql of wave pixels 32 t + 8 qk + j, j = 0..7
     const int ql = lane & 15, qk = lane >> 4;
@@ -1123,10 +1128,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
                 if (a != 0.f) {
                     if (DET) {  // integer adds commute: order-independent sums (a is already in fixed-point units)
-                        // (the design bound is |a| <= ~2^51 per flush, so sums of 2^11 flushes stay below 2^63; a
-                        // flush beyond 2^62 breaks it -- counted, and k_preproc_bwd then poisons the call's
-                        // gradients with NaN instead of returning silently wrapped sums)
-                        if (!(fabsf(a) <= 0x1p62f)) atomicAdd(det_sat, 1u);
+                        // (an accumulator takes at most one flush per tile of its view -- one work item per tile
+                        // in this mode, an entry once per tile list -- so |a| <= det_lim = 2^62 / 2^ceil(log2 T)
+                        // keeps every sum below 2^62 whatever the flushes' signs; the design value is |a| <= ~2^51
+                        // per flush. A flush beyond the bound is counted and k_preproc_bwd then poisons the call's
+                        // gradients with NaN instead of returning possibly wrapped sums)
+                        if (!(fabsf(a) <= det_lim)) atomicAdd(det_sat, 1u);
                         atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
                                   (unsigned long long)__float2ll_rn(fminf(fmaxf(a, -9.0e18f), 9.0e18f)));
                     } else {
@@ -1445,7 +1452,7 @@ int launch_render_bwd(const Dims &d, const float *gaussians, const float *cam_vi
         LGM_LAUNCH("k_det_seed_max", st, (smax<<<(unsigned)min(d.BV * d.T, DET_MAX_WGS), 256, 0, st>>>(
                                              d, (const float *)(ws + L.final_T), bg, (const float4 *)(ws + L.cfin),
                                              d_image, d_depth, d_alpha, (const unsigned char *)(ws + L.cmask),
-                                             det_max)));
+                                             det_max, (unsigned *)(ws + L.misc) + 13)));
     }
     auto pick = [&](auto depth_tag) {
         constexpr bool DP = decltype(depth_tag)::value;

@@ -84,6 +84,11 @@ def warm_up(step: Callable[[], None], steps: int, sync: Callable[[], None], info
     import math
     import time
     steps = max(1, steps)
+    # the first call carries one-time costs (library load, the workspace's first allocation, autograd setup): it is
+    # kept out of the rate estimate, else a slow first call makes W steps "long enough" and the timed loop starts
+    # on cold clocks (BENCH_r04's pool: 5 warmup steps, timed mean 6.5 % above the same run's median step)
+    step()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -95,23 +100,49 @@ def warm_up(step: Callable[[], None], steps: int, sync: Callable[[], None], info
     for _ in range(extra):
         step()
     sync()
-    return steps + extra
+    return 1 + steps + extra
 
 
 def timed_steps(step: Callable[[], None], steps: int, info: RankInfo, sync: Callable[[], None],
-                device=None) -> float:
+                device=None, stamps: dict | None = None) -> float:
     """Time exactly `steps` calls of step(): barrier + sync on both sides, wall time maxed over ranks (seconds).
     Python's collector is left as it is: a full collection right before the loop made the next few dozen single-scene
     steps ~16 us slower on the GPU (profiles/r04/diag_host: 225 -> 241 us per step, host work unchanged), and pausing
-    it for the loop measured slower too (profiles/r04/s3_gc_paused)."""
+    it for the loop measured slower too (profiles/r04/s3_gc_paused).
+
+    stamps (a dict, CUDA devices only): also records, inside the timed loop, each step's host enqueue time and an
+    event after each step on the current stream, and fills stamps with 'host_ms' (per step), 'gpu_ms' (event to
+    event; the first span starts at t0, so it holds the first step's launch latency) and 'tail_ms' (last event to
+    the end of the final sync, host clock) -- where a slow loop's time went, at the cost of one event record per
+    step."""
+    evs = None
+    if stamps is not None:
+        import torch
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        host = [0.0] * steps
     barrier(info)
     sync()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    if evs is None:
+        for _ in range(steps):
+            step()
+    else:
+        evs[0].record()
+        for i in range(steps):
+            h = time.perf_counter()
+            step()
+            host[i] = time.perf_counter() - h
+            evs[i + 1].record()
     sync()
+    t1 = time.perf_counter()
     barrier(info)
-    return max_over_ranks(time.perf_counter() - t0, info, device)
+    el = t1 - t0
+    if evs is not None:
+        gpu = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+        stamps.update(host_ms=[round(1e3 * h, 4) for h in host], gpu_ms=[round(g, 4) for g in gpu],
+                      loop_ms=round(1e3 * el, 4), gpu_sum_ms=round(sum(gpu), 4),
+                      tail_ms=round(1e3 * el - sum(gpu), 4))
+    return max_over_ranks(el, info, device)
 
 
 def _spawned_rank(local_rank, world, port, target, args):

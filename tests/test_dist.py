@@ -251,5 +251,5 @@ def test_warm_up_matches_call_counts_over_ranks(tmp_path):
     calls on every rank, so a step holding a collective cannot deadlock."""
     res = _run("warmup", tmp_path)
     ns = [int(r["n"]) for r in res]
-    assert ns[0] == ns[1] and ns[0] >= 2
+    assert ns[0] == ns[1] and ns[0] >= 3  # the untimed first call + W = 2
     assert ns[0] * 0.016 >= 0.1 * 0.8  # the collective paces both ranks at the slow one's 16 ms per step

@@ -139,6 +139,30 @@ def test_repeated_backward_retain_graph(cuda):
     assert rel_l2(second.cpu().numpy(), first.cpu().numpy()) < 1e-5
 
 
+def test_deterministic_saturation_poisons_and_resets(cuda):
+    """LGM_RENDER_DETERMINISTIC's overflow guard (render_raster.hip k_render_bwd flush): a flush above the per-flush
+    bound (2^62 / 2^ceil(log2 tiles): no sum of one flush per tile can wrap int64) is counted and k_preproc_bwd
+    poisons the call's gradients with NaN. The lgm_diag test hook lowers the bound to 2^1 to force that path; a
+    retain_graph repeat of the same forward without the hook (LGM_RENDER_BACKWARD_AGAIN) must not inherit the
+    count (k_det_seed_max clears it) and equals a clean backward bitwise."""
+    from lgm_amd import _native
+    g, cv, cvp = scene(N=3000, V=2, seed=5)
+    gd = g.to(cuda).requires_grad_(True)
+    args = (cv.to(cuda), cvp.to(cuda), torch.ones(3, device=cuda), TAN, TAN, 64, 64)
+    w = torch.randn((1, 2, 3, 64, 64), generator=torch.Generator().manual_seed(3)).to(cuda)
+    img, _, alp = rasterize(gd, *args, deterministic=True)
+    loss = (img * w).sum() + alp.sum()
+    with _native.diagnostics(det_limit_log2=1):
+        (poisoned,) = torch.autograd.grad(loss, gd, retain_graph=True)
+    (again,) = torch.autograd.grad(loss, gd)
+    img2, _, alp2 = rasterize(gd, *args, deterministic=True)
+    (clean,) = torch.autograd.grad((img2 * w).sum() + alp2.sum(), gd)
+    torch.cuda.synchronize()
+    assert torch.isnan(poisoned).all()
+    assert torch.isfinite(again).all() and again.abs().sum().item() > 0
+    assert torch.equal(again, clean)
+
+
 def test_cfg2_full_size_forward(cuda, oracle_mod):
     # BASELINE config 2: 50k Gaussians, 1 camera, 256^2, fwd only (seed 0)
     g, cv, cvp = scene(N=50000, V=1, seed=0)

@@ -112,13 +112,21 @@ int lgm_render_pixel_state(int B, int V, int N, int H, int W, const void *worksp
  *   accumulated in fp64 (float mode). Invisible records: rects (0, 0). */
 int lgm_render_records(int B, int V, int N, int H, int W, const void *workspace, size_t workspace_bytes,
                        long long pair_capacity, float *P_out, float *Q_out, unsigned *rects_out, void *stream);
+/* lgm_render_needle_flags: the float mode's needle decision (render_common.h rec_needle: conic condition
+ * (A + C)^2 / (AC - B^2) above 300, or not positive definite; the record's conic partials then go to fp64
+ * accumulators) evaluated on n caller-given DEVICE triples abc [n,3] = (A', B', C') as a record stores them ->
+ * flags_out [n] (DEVICE u8, 1 = needle). The binning and the backward's flush take this same decision on the stored
+ * record; a test pins it to separately rounded IEEE operations (no FP contraction) near the threshold. */
+int lgm_render_needle_flags(long long n, const float *abc, unsigned char *flags_out, void *stream);
 
 /* Diagnostics: when diag->render_counters (a DEVICE uint64 buffer, caller-zeroed) is set, that call's render kernels
  * record per-workgroup timelines in it: [0..7] section cycles of the LGM_BWD_STAMPS diagnostic build (else unused);
  * then 8 entries per tile t (B*V*T tiles): s_memrealtime stamps (100 MHz) [8+8t] fwd start, [+1] fwd end,
  * [+2], [+3] the start / end of preprocess-backward workgroup t (t < its grid), [+4] sort start, [+5] sort end,
- * [+6] the tile's binned list length, [+7] list entries the forward staged (low 32 bits) and wave 0's
- * 4-entry steps (high 32 bits); then 8 entries per binning workgroup
+ * [+6] the tile's binned list length (low 32 bits; k_sort writes it, k_render_fwd rewrites it with the HW_ID of the
+ * wave that composited the tile -- SE / CU / SIMD / slot -- in the high 32 bits), [+7] list entries the forward
+ * staged (bits 0-31), wave 0's 4-entry steps (bits 32-55) and the XCC_ID of the XCD it ran on (bits 56-63); then 8
+ * entries per binning workgroup
  * (room for B*V*ceil(N/512); the binning launch uses its first B*ceil(V/3)*ceil(N/512)): phase stamps [0] start,
  * [1] preprocessed, [2] tile tests done, [3] reserved, [4] end, [5] its binned pairs, [6] HW_ID and [7] XCC_ID of where it
  * ran; then 4 entries per backward work item (at most 3*B*V*tiles + 16 items: one per tile, rounded up to 8, and

@@ -449,8 +449,9 @@ constexpr int LDK_PAD = 16, FWD_WPE = 3, BWD_WPE = 2;
 // VGPRs; 3 at the compiler's own 136): bench level k_attn_dkdv 636 -> 625 us (profiles/r04/ab_session_f; the
 // forward split the same way ran 412 -> 435 us and stays whole)
 constexpr int DKDV_WPE32 = 4;
-// The softmax's affine parts ride on the MFMAs: the register operand (Q in the forward and dQ kernels, K in dK/dV)
-// is pre-scaled by scale * log2(e) (rounded to the 16-bit type once), so S comes out in log2 units, and the S / dP
+// The softmax's affine parts ride on the MFMAs: Q is pre-scaled by scale * log2(e) (rounded to the 16-bit type once;
+// in registers in the forward and dQ kernels, as a second LDS image in dK/dV -- all three recompute P from the same
+// rounded operands), so S comes out in log2 units, and the S / dP
 // accumulators start at -m (-lse') and -delta of their rows, so exp2's argument and dS's (dP - delta) factor leave
 // the MFMA ready: no per-score fma or subtract (profiles/r04: D = 32 fwd / dQ / dK,dV measured in DESIGN.md §4).
 constexpr float ATT_THR = 8.0f;  // forward: the row reference m is raised only when a score exceeds it by more than
@@ -647,6 +648,18 @@ struct TileLoader {  // one 64-row tile of up to two [tokens][ld] tensors, CH 16
             *reinterpret_cast<uint4 *>(tb + r * ldt + col) = b[cc];
         }
     }
+    // a second image of the first tensor, each element times c rounded to T (as prescale() rounds a register operand)
+    __device__ __forceinline__ void store_scaled_a(T *tc, int ldt, float c) {
+#pragma unroll
+        for (int cc = 0; cc < CH; cc++) {
+            const int ci = threadIdx.x + cc * NT, r = ci / (D / 8), col = (ci - r * (D / 8)) * 8;
+            const T *e = reinterpret_cast<const T *>(&a[cc]);
+            T o[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) o[j] = (T)((float)e[j] * c);
+            *reinterpret_cast<uint4 *>(tc + r * ldt + col) = *reinterpret_cast<const uint4 *>(o);
+        }
+    }
 };
 
 // dK, dV: grid (ceil(L / (64 KS)), B*H); wavefront w owns keys k0 + 16 s + (lane & 15), s < KS.
@@ -662,6 +675,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     using V8 = typename Ty<DT>::V8;
     constexpr int LDK = D + LDK_PAD;
     __shared__ __attribute__((aligned(16))) T Qs[2][64 * LDK];
+    __shared__ __attribute__((aligned(16))) T Qc[2][64 * LDK];  // Q * scale * log2(e), rounded: the S operand
     __shared__ __attribute__((aligned(16))) T Os[2][64 * LDK];
     __shared__ float sl[2][64], sd[2][64];
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -676,7 +690,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
         const int kr = k0 + 16 * s + r16;
         load_yfrag<DT, D>(kf[s], k + base + (long long)kr * ld, kr < L, g);
         load_yfrag<DT, D>(vf[s], v + base + (long long)kr * ld, kr < L, g);
-        prescale<DT, D / 32>(kf[s].v, c);  // S in log2 units
+#ifdef LGM_AB_KPRE
+        prescale<DT, D / 32>(kf[s].v, c);
+#endif
     }
     f32x4 dka[KS][D / 16], dva[KS][D / 16];
 #pragma unroll
@@ -695,6 +711,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     };
     auto store_rows2 = [&](int buf) {
         ld_.store(Qs[buf], Os[buf], LDK);
+        // S from the same rounded operand as k_attn_fwd2 / k_attn_dq2 (Q * c; K unscaled), so the P recomputed here
+        // is the P whose row sums gave lse; dK's product keeps the unscaled image
+#ifndef LGM_AB_KPRE
+        ld_.store_scaled_a(Qc[buf], LDK, c);
+#endif
         if (tid < 64) {  // stored negated: the accumulator inits
             // (the row index recomputed here: the two LDS addresses hoisted out of the query loop were spilled at the
             // 128-VGPR cap, and their scratch reloads sat on wave 0's path to every tile's barrier)
@@ -711,7 +732,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     for (int qb = 0; qb < L; qb += 64) {
         const bool more = qb + 64 < L;
         if (more) load_rows2(qb + 64);
-        const T *Qt = Qs[cur], *Ot = Os[cur];
+        const T *Qt = Qs[cur], *Qct = Qc[cur], *Ot = Os[cur];
         // the tile's two 32-query halves one after the other (S / dP of subs 2t, 2t + 1, then their dV / dK
         // products): half the score registers live at once (dK,dV at D = 32 fits 4 waves per SIMD instead of 3)
 #pragma unroll
@@ -723,7 +744,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
                 V8 qr[D / 32], orr[D / 32];
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
+#ifdef LGM_AB_KPRE
                     qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+#else
+                    qr[cc] = *reinterpret_cast<const V8 *>(Qct + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+#endif
                     orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
                 }
                 // (the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i, read as stored)

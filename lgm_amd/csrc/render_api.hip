@@ -43,6 +43,15 @@ int check_common(int B, int V, int N, int H, int W, const void *g, const void *c
 
 bool capacity_ok(long long cap) { return cap <= 0x7fffffffLL; }
 
+// lgm_render_needle_flags: render_common.h rec_needle (the decision the binning and the backward's flush both take
+// on a stored record) evaluated on caller-given (A', B', C')
+__global__ __launch_bounds__(256) void k_needle_flags(long long n, const float *__restrict__ abc,
+                                                      unsigned char *__restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    out[i] = lgm::rec_needle(abc[3 * i], abc[3 * i + 1], abc[3 * i + 2]) ? 1 : 0;
+}
+
 // Inspection kernels (lgm_render_tile_lists / lgm_render_pixel_state): plain copies out of the workspace.
 __global__ __launch_bounds__(256) void k_tile_counts(int M, long long slot_stride, const int *__restrict__ tile_start,
                                                      const int *__restrict__ tile_count, int *__restrict__ out) {
@@ -300,6 +309,18 @@ int lgm_render_records(int B, int V, int N, int H, int W, const void *workspace,
             return LGM_E_HIP;
         }
     }
+    return LGM_OK;
+}
+
+int lgm_render_needle_flags(long long n, const float *abc, unsigned char *flags_out, void *stream) {
+    lgm::clear_error();
+    if (n < 0 || (n > 0 && (!abc || !flags_out))) {
+        lgm::set_error("invalid needle-flag arguments");
+        return LGM_E_INVALID;
+    }
+    if (n == 0) return LGM_OK;
+    hipStream_t st = (hipStream_t)stream;
+    LGM_LAUNCH("k_needle_flags", st, (k_needle_flags<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, abc, flags_out)));
     return LGM_OK;
 }
 

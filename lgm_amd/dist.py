@@ -210,9 +210,12 @@ class GradAccumulator:
     steps - 1 micro-steps run their backward inside DDP's no_sync() (gradients summed locally, no all-reduce), the
     last one all-reduces the summed gradients once; backward() scales the loss by 1 / steps (accelerate.backward)
     and `sync_gradients` says when the clip and the optimizer step apply (accelerate skips both otherwise).
+    The last batch of the data forces a sync and restarts the count (accelerate's sync_with_dataloader default:
+    an epoch whose length `steps` does not divide neither carries its leftover micro-batch gradients into the next
+    epoch nor shifts the next epoch's sync phase); pass last=True for it.
         acc = GradAccumulator(ddp, steps)
-        for batch in data:
-            with acc.accumulate():
+        for i, batch in enumerate(loader):
+            with acc.accumulate(last=i == len(loader) - 1):
                 loss = ...; acc.backward(loss)
                 if acc.sync_gradients: clip; opt.step(); opt.zero_grad()"""
 
@@ -221,10 +224,13 @@ class GradAccumulator:
             raise ValueError("gradient accumulation steps must be >= 1")
         self.model, self.steps, self.count, self.sync_gradients = model, int(steps), 0, True
 
-    def accumulate(self):
+    def accumulate(self, last: bool = False):
         import contextlib
-        self.count += 1
-        self.sync_gradients = self.count % self.steps == 0
+        if last:  # (accelerate GradientState.end_of_dataloader: sync, and the next micro-step counts from 1)
+            self.count, self.sync_gradients = 0, True
+        else:
+            self.count += 1
+            self.sync_gradients = self.count % self.steps == 0
         no_sync = getattr(self.model, "no_sync", None)
         return contextlib.nullcontext() if self.sync_gradients or no_sync is None else no_sync()
 

@@ -31,9 +31,9 @@ with _native.diagnostics(render_counters=cnt):
     torch.autograd.backward([out["image"], out["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
     torch.cuda.synchronize()
 c = cnt.tolist()
-names = ["fwd_wave_iters", "fwd_contribs", "bwd_wave_iters", "bwd_contribs", "bwd_dense", "bwd_sparse",
-         "fwd_entries_staged", "fwd_max_wave_iters"]
-res = dict(zip(names, c[:8]))
+# [0..7] hold only the LGM_BWD_STAMPS build's backward section cycles ([2..6], scripts/diag_bwd_stamps.py reads them);
+# the forward no longer writes aggregate counters there (include/lgm_render.h)
+res = {"bwd_section_cycles_stamps_build": c[2:7]} if any(c[:8]) else {}
 import numpy as np  # noqa: E402
 tl = np.array(c[8:8 + 8 * M], dtype=np.int64).reshape(M, 8)
 nl = tl[:, 6] & 0xFFFFFFFF
@@ -57,8 +57,9 @@ for name, (a, b) in {"fwd": (0, 1), "preproc_bwd": (2, 3), "sort": (4, 5)}.items
     res[f"{name}_wg_sum_us"] = float(dur.sum())
     order = np.argsort(-dur)[:5]
     res[f"{name}_slowest_tiles"] = [(int(np.nonzero(ok)[0][i]), float(dur[i])) for i in order]
-res["fwd_lane_util"] = c[1] / max(1, 64 * c[0])
-res["bwd_lane_util"] = c[3] / max(1, 64 * c[2])
+st7 = np.array(c[8:8 + 8 * M], dtype=np.int64).reshape(M, 8)[:, 7]
+res["fwd_entries_staged"] = int((st7 & 0xFFFFFFFF).sum())  # [+7] low 32 bits per tile
+res["fwd_wave0_steps"] = int(((st7 >> 32) & 0xFFFFFF).sum())  # [+7] bits 32-55
 print(json.dumps(res, indent=1))
 os.makedirs("gpurun_out", exist_ok=True)
 json.dump(res, open(f"gpurun_out/counters_B{B}.json", "w"), indent=1)

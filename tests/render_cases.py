@@ -48,3 +48,32 @@ def rel_l2(a, b) -> float:
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def near_threshold_records(n_base=400, span=24, seed=0):
+    """(A', B', C') float32 triples as a record stores them (render_common.h rec_p / rec_q) whose conic condition
+    (A' + C')^2 / (A'C' - B'^2 / 4) lies within a few ulp of rec_needle's threshold 300, and for each the needle
+    decision of the separately rounded expression and of its two possible FMA contractions (fma(A', C', -bb) and
+    fma(-B'/4, B', A'C'), each one rounding of the exact value)."""
+    from fractions import Fraction as Fr
+    f32 = np.float32
+    rng = np.random.default_rng(seed)
+    recs, dec = [], []
+    for _ in range(n_base):
+        Ap = f32(-np.exp(rng.uniform(np.log(0.01), np.log(50.0))))
+        Cp = f32(Ap * f32(np.exp(rng.uniform(np.log(0.05), np.log(20.0)))))
+        sac = f32(Ap + Cp)
+        b2 = 4.0 * (float(Ap) * float(Cp) - float(sac) ** 2 / 300.0)  # B' at condition 300 exactly
+        if b2 <= 0:
+            continue
+        b0 = np.array([np.sqrt(b2)], f32).view(np.int32)[0]
+        for k in range(-span, span + 1):  # B' stepped by k ulp
+            Bp = np.array([b0 + k], np.int32).view(f32)[0]
+            q = f32(f32(0.25) * Bp)
+            bb, ac = f32(q * Bp), f32(Ap * Cp)
+            dqs = (f32(ac - bb), f32(float(Fr(float(Ap)) * Fr(float(Cp)) - Fr(float(bb)))),
+                   f32(float(Fr(float(ac)) - Fr(float(q)) * Fr(float(Bp)))))
+            ss = f32(sac * sac)
+            recs.append((Ap, Bp, Cp))
+            dec.append([not (ss <= f32(f32(300.0) * x)) for x in dqs])
+    return np.array(recs, f32), np.array(dec, bool)

@@ -60,5 +60,5 @@ def test_no_process_wide_switches():
         txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
         for name, args in re.findall(r"\b(lgm_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", txt):
             if "void *stream" in args and name not in ("lgm_render_tile_lists", "lgm_render_pixel_state",
-                                                              "lgm_render_records"):
+                                                              "lgm_render_records", "lgm_render_needle_flags"):
                 assert args.rstrip().endswith("const lgm_diag *diag"), name

@@ -253,3 +253,21 @@ def test_warm_up_matches_call_counts_over_ranks(tmp_path):
     ns = [int(r["n"]) for r in res]
     assert ns[0] == ns[1] and ns[0] >= 3  # the untimed first call + W = 2
     assert ns[0] * 0.016 >= 0.1 * 0.8  # the collective paces both ranks at the slow one's 16 ms per step
+
+
+def test_gradient_accumulation_end_of_data():
+    """GradAccumulator at the end of the data (accelerate's sync_with_dataloader): with steps = 3 and 4 batches per
+    epoch, the 4th (last) batch syncs and restarts the count, so every epoch syncs at batches 3 and 4 and no
+    micro-batch gradient is left unsynced between epochs. Without a process group no_sync does not apply."""
+    m = torch.nn.Linear(4, 2)
+    acc = D.GradAccumulator(m, 3)
+    pattern = []
+    for epoch in range(3):
+        for i in range(4):
+            with acc.accumulate(last=i == 3):
+                acc.backward(m(torch.ones(1, 4)).sum())
+                pattern.append(acc.sync_gradients)
+                if acc.sync_gradients:
+                    m.zero_grad()
+    assert pattern == [False, False, True, True] * 3
+    assert acc.count == 0

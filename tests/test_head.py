@@ -1,7 +1,7 @@
 """Fused Gaussian head (lgm_amd/head.py, include/lgm_head.h): LGM.forward_gaussians' epilogue
 (core/models.py:95-117) against its fp32 torch restatement (oracle/head_ref.py), forward and backward.
 
-Tolerances (floating point): Gaussians and all gradients (dx, d_weight, d_bias) within max(1e-5, 2 x the fp32
+Tolerances (floating point): Gaussians and all gradients (dx, d_weight, d_bias) within max(1e-5, 1.25 x the fp32
 restatement's own error) relative L2 of the restatement evaluated in fp64, for fp32 input; bf16 input: the same bf16 values fed to the restatement in fp32, dx compared
 after bf16 rounding (2e-3). The kernels accumulate in a fixed order: two backward runs are bitwise identical."""
 import numpy as np
@@ -11,7 +11,7 @@ import torch
 from lgm_amd import _native
 from lgm_amd.head import GaussianHead, gaussian_head
 from oracle.head_ref import forward_gaussians_epilogue
-from tests.render_cases import rel_l2
+from tests.render_cases import GRAD_FACTOR, rel_l2
 
 
 def _inputs(B, V, h, w, seed, dtype=torch.float32):
@@ -57,7 +57,8 @@ def _torch_ref(x, conv, d, B, V, dtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,V,h,w", [(1, 4, 64, 64), (2, 3, 17, 23), (1, 6, 160, 160), (3, 1, 1, 1)])
 def test_head_fp32_vs_torch(cuda, B, V, h, w):
-    """GPU vs the restatement evaluated in fp64, bar max(1e-5, 2 x the fp32 restatement's own error): the
+    """GPU vs the restatement evaluated in fp64, bar max(1e-5, 1.25 x the fp32 restatement's own error, the render
+    tests' GRAD_FACTOR): the
     rotation's normalisation over N Gaussians (a 153,600-term sum at cfg4) leaves torch's fp32 CPU reduction
     ~1.4e-5 off, so the fp32 restatement cannot be the bar there."""
     x, conv, d = _inputs(B, V, h, w, seed=B * 100 + V * 10 + h)
@@ -74,8 +75,10 @@ def test_head_fp32_vs_torch(cuda, B, V, h, w):
            "db": cg.bias.grad.cpu().numpy()}
 
     def check(name, a, b32, b64):
-        bar = max(1e-5, 2.0 * rel_l2(b32, b64))
+        e32 = rel_l2(b32, b64)
+        bar = max(1e-5, GRAD_FACTOR * e32)
         e = rel_l2(a, b64)
+        print(f"head {B}x{V}x{h}x{w} {name}: GPU {e:.3e}, fp32 restatement {e32:.3e}, bar {bar:.3e}")
         assert e < bar, f"{name}: GPU vs fp64 {e:.3e}, bar {bar:.3e}"
 
     for k in gpu:

@@ -15,7 +15,7 @@ import torch
 
 from lgm_amd import gs as lgs
 from lgm_amd.gs import rasterize
-from tests.render_cases import TAN, grad_bar, rel_l2, scene, upstream
+from tests.render_cases import TAN, grad_bar, near_threshold_records, rel_l2, scene, upstream
 
 pytestmark = pytest.mark.gpu
 
@@ -250,6 +250,21 @@ def test_fused_clamp_matches_torch_clamp(cuda):
     assert 0.01 < frac < 0.9, frac  # the clamp is actually exercised
     assert torch.equal(outs[True][0], raw.clamp(0, 1))
     assert rel_l2(outs[True][1].cpu().numpy(), outs[False][1].cpu().numpy()) < 1e-5
+
+
+def test_needle_decision_is_contraction_free(cuda):
+    """rec_needle on the GPU (lgm_render_needle_flags: the function the binning's flag and the backward flush's
+    re-derivation both call, render_bin.hip / render_raster.hip) decides every near-threshold record exactly as the
+    separately rounded IEEE expression, including those where an FMA contraction would flip it."""
+    from lgm_amd import _native
+    recs, dec = near_threshold_records()
+    abc = torch.from_numpy(recs).to(cuda)
+    flags = torch.empty(len(recs), dtype=torch.uint8, device=cuda)
+    _native.check(_native.lib().lgm_render_needle_flags(len(recs), _native.ptr(abc), _native.ptr(flags),
+                                                        _native.stream_of(cuda)), "lgm_render_needle_flags")
+    got = flags.cpu().numpy().astype(bool)
+    assert np.array_equal(got, dec[:, 0]), f"{int((got != dec[:, 0]).sum())} decisions differ"
+    assert (got != dec[:, 1]).any() or (got != dec[:, 2]).any()
 
 
 def test_needle_flag_is_a_function_of_the_stored_record(cuda):

@@ -71,6 +71,12 @@ def main():
     seeded = [  # name, ctor kwargs, input shape: LGM's real channel widths, 16 heads
         ("mv_c512_h16_f4_l4096", dict(dim=512, num_heads=16, num_frames=4, skip_scale=0.5 ** 0.5), (4, 512, 32, 32)),
         ("mv_c1024_h16_f4_l256", dict(dim=1024, num_heads=16, num_frames=4, skip_scale=0.5 ** 0.5), (4, 1024, 8, 8)),
+        # BASELINE config 4, LGM 'big' (6 input views at 320, core/unet.py:35-49 with num_frames=6): its three
+        # attention levels exactly -- C = 512 at 40^2 (L = 9600, D = 32), C = 1024 at 20^2 (L = 2400) and 10^2 (L = 600)
+        ("mv_c512_h16_f6_l9600", dict(dim=512, num_heads=16, num_frames=6, skip_scale=0.5 ** 0.5), (6, 512, 40, 40)),
+        ("mv_c1024_h16_f6_l2400", dict(dim=1024, num_heads=16, num_frames=6, skip_scale=0.5 ** 0.5),
+         (6, 1024, 20, 20)),
+        ("mv_c1024_h16_f6_l600", dict(dim=1024, num_heads=16, num_frames=6, skip_scale=0.5 ** 0.5), (6, 1024, 10, 10)),
     ]
     only = set(sys.argv[1:])  # optional: regenerate only the named cases
     for name, kw, shape in seeded:

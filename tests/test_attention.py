@@ -70,10 +70,12 @@ def _module(meta):
 
 
 def test_golden_present():
-    assert len(GOLDEN) >= 10
+    assert len(GOLDEN) >= 13
     names = [os.path.basename(p) for p in GOLDEN]
     # LGM's real channel widths with 16 heads (core/unet.py:113-206): D = 32 at L = 4096 and D = 64
     assert "attn_mv_c512_h16_f4_l4096.npz" in names and "attn_mv_c1024_h16_f4_l256.npz" in names
+    # BASELINE config 4's three MVAttention levels exactly (num_frames = 6: L = 9600 at C = 512, 2400 and 600 at 1024)
+    assert {"attn_mv_c512_h16_f6_l9600.npz", "attn_mv_c1024_h16_f6_l2400.npz", "attn_mv_c1024_h16_f6_l600.npz"} <= set(names)
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=lambda p: os.path.basename(p)[5:-4])

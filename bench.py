@@ -288,6 +288,57 @@ def attention_bench(dev, steps: int = 10):
             "torch_sdpa_tflops": round(flops / ms_sdpa / 1e9, 1) if ms_sdpa else None}
 
 
+def mva_level_bench(dev, steps: int = 10):
+    """One whole MVAttention block of the bench level (core/unet.py:11-49: GroupNorm, token permute, qkv Linear,
+    attention, proj Linear, permute back, residual, skip_scale; C = 512, 32x32 x 4 views, 16 heads, 8 objects),
+    fwd+bwd under bf16 autocast as LGM trains: the fused HIP layout passes (lgm_mva_*, forward and backward) against
+    the same module on upstream's torch ops around the same HIP attention core (fused=False). Per-kernel times of
+    the fused step from a separate pass."""
+    import torch
+
+    from lgm_amd import _native
+    from lgm_amd import dist as Dist
+    from lgm_amd.attention import MVAttention
+    B, F, C, HH, WW = 8, 4, 512, 32, 32
+    torch.manual_seed(3)
+    m = MVAttention(C, 16, num_frames=F, skip_scale=0.5 ** 0.5).to(dev)
+    x = (torch.randn(B * F, C, HH, WW, device=dev) * 2 + 0.3).requires_grad_(True)
+    gy = torch.randn(B * F, C, HH, WW, device=dev)
+
+    def step():
+        x.grad = None
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(x)
+        y.backward(gy)
+
+    def timed():
+        Dist.warm_up(step, 1, torch.cuda.synchronize)
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for _ in range(steps):
+            step()
+        en.record()
+        torch.cuda.synchronize()
+        return st.elapsed_time(en) / steps
+
+    res = {"workload": f"MVAttention block C={C} {HH}x{WW} x {F} views, 16 heads, {B} objects, fwd+bwd, bf16 autocast "
+                       "(GroupNorm + layout + qkv/proj Linear + attention + residual)"}
+    for fused in (True, False):
+        m.fused = fused
+        res["fused_ms" if fused else "torch_layout_ms"] = round(timed(), 4)
+    m.fused = True
+    prof = _native.KernelProfiler()
+    with prof:
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+    res["kernels"] = {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in prof.summary().items()
+                      if k.startswith("k_mva")}
+    prof.close()
+    return res
+
+
 def cfg2_bench(dev, steps):
     """BASELINE config 2: 50k Gaussians, 1 camera, 256^2, RGB+alpha forward only (bg = ones, seed 0)."""
     import torch
@@ -634,6 +685,7 @@ def run(args):
             result["cfg4"] = cfg4_bench(dev, max(3, args.steps // 10))
         if not args.no_attention:
             result["attention"] = attention_bench(dev)
+            result["mva_level"] = mva_level_bench(dev)
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(g3.detach().cpu(), cv[None], cvp[None], tan, bg3, d3_img, d3_alpha,
                                                   args.cpu_seconds)

@@ -62,6 +62,27 @@ int lgm_mva_norm_tokens(int dtype_x, int dtype_tok, int B, int F, int C, int HW,
 int lgm_mva_tokens_out(int dtype_y, int dtype_res, int dtype_out, int B, int F, int C, int HW, const void *y,
                        const void *res, float skip, void *out, void *stream, const lgm_diag *diag);
 
+/* Backward of the two passes above (autograd through core/unet.py:40-48), replacing torch's permute copies, cast,
+ * native_group_norm_backward and the residual's gradient sum:
+ *
+ * lgm_mva_tokens_out_backward: g = d_out * scale rounded to d_out's dtype (scale = skip_scale with a residual, 1
+ * without: torch's `d_out * skip`); d_y [B, F*HW, C] (dtype_dy) = g in the token layout, and, if d_res is not NULL,
+ * d_res [B*F, C, HW] (dtype_dres) = g.
+ *
+ * lgm_mva_norm_tokens_backward: the GroupNorm backward (torch's fused parameters: dx = rstd gamma dy + c2 x + c3 per
+ * (sample, group); dgamma_c = sum_n (sum dy x - mean sum dy) rstd, dbeta_c = sum dy) of dy = d_tokens read back
+ * from the token layout, with mean / rstd from lgm_mva_norm_tokens; dx [B*F, C, HW] (dtype_x) = that + d_res (the
+ * residual's gradient, dtype_x, NULL = none) in one rounding. dx, dgamma, dbeta (fp32 [C]) may be NULL. Every sum is
+ * in a fixed order (bitwise reproducible). Channels per group <= 256. workspace: lgm_mva_backward_workspace_size. */
+size_t lgm_mva_backward_workspace_size(int B, int F, int C, int HW, int groups);
+int lgm_mva_tokens_out_backward(int dtype_dout, int dtype_dy, int dtype_dres, int B, int F, int C, int HW,
+                                const void *d_out, float scale, void *d_y, void *d_res, void *stream,
+                                const lgm_diag *diag);
+int lgm_mva_norm_tokens_backward(int dtype_x, int dtype_tok, int B, int F, int C, int HW, int groups, const void *x,
+                                 const float *gamma, const float *mean, const float *rstd, const void *d_tokens,
+                                 const void *d_res, void *dx, float *dgamma, float *dbeta, void *workspace,
+                                 size_t workspace_bytes, void *stream, const lgm_diag *diag);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,11 @@ SIGNATURES = {
                                      _vp, _vp, _vp, _vp, _c_size, _vp, _vp]),
     "lgm_mva_tokens_out": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _vp,
                                     _vp, _vp]),
+    "lgm_mva_backward_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
+    "lgm_mva_tokens_out_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_float, _vp,
+                                             _vp, _vp, _vp]),
+    "lgm_mva_norm_tokens_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp,
+                                              _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp, _vp]),
     "lgm_render_forward_loss": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_float,
                                          _c_float, _c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _c_ll, _c_int,
                                          _vp, _vp]),

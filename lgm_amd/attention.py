@@ -147,7 +147,9 @@ def _autocast_dtype(dev_type: str):
 
 class _NormTokens(torch.autograd.Function):
     """GroupNorm of x [B*F, C, H, W] straight into MVAttention's token layout [B, F*H*W, C] (core/unet.py:40-42) in
-    one HIP pass (lgm_mva_norm_tokens). Backward: torch's GroupNorm backward on the un-permuted gradient."""
+    one HIP pass (lgm_mva_norm_tokens). Also returns x itself (an alias) for the residual of core/unet.py:47, so the
+    residual's gradient arrives here and the backward (lgm_mva_norm_tokens_backward) adds it to the GroupNorm's dx
+    in the same pass, instead of autograd summing the two afterwards."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, F: int, groups: int, eps: float, tok_dtype):
@@ -168,19 +170,33 @@ class _NormTokens(torch.autograd.Function):
                   "lgm_mva_norm_tokens")
         ctx.save_for_backward(x, weight, mean, rstd)
         ctx.shape = (B, F, C, H, W, groups)
-        return tok
+        ctx.set_materialize_grads(False)
+        return tok, x
 
     @staticmethod
-    def backward(ctx, d_tok):
+    def backward(ctx, d_tok, d_res):
         x, weight, mean, rstd = ctx.saved_tensors
         B, F, C, H, W, groups = ctx.shape
-        g = d_tok.reshape(B, F, H, W, C).permute(0, 1, 4, 2, 3).reshape(B * F, C, H, W).float().contiguous()
-        mask = [ctx.needs_input_grad[0], weight is not None and ctx.needs_input_grad[1],
-                weight is not None and ctx.needs_input_grad[2]]
-        dx, dw, db = torch.ops.aten.native_group_norm_backward(g, x.float(), mean, rstd,
-                                                               None if weight is None else weight.float(), B * F, C,
-                                                               H * W, groups, mask)
-        dx = None if dx is None else dx.to(x.dtype)
+        need_x = ctx.needs_input_grad[0]
+        need_w = weight is not None and ctx.needs_input_grad[1]
+        need_b = weight is not None and ctx.needs_input_grad[2]
+        if d_tok is None:  # only the residual's gradient reached x
+            return (d_res if need_x else None), None, None, None, None, None, None
+        d_tok = d_tok.contiguous()
+        if d_res is not None:
+            d_res = d_res.to(x.dtype).contiguous()
+        dx = torch.empty_like(x) if need_x else None
+        dw = torch.empty(C, device=x.device, dtype=torch.float32) if need_w else None
+        db = torch.empty(C, device=x.device, dtype=torch.float32) if need_b else None
+        L_ = nat.lib()
+        ws_bytes = L_.lgm_mva_backward_workspace_size(B, F, C, H * W, groups)
+        ws = torch.empty(max(ws_bytes, 1), device=x.device, dtype=torch.uint8)
+        gamma = None if weight is None else weight.detach().float().contiguous()
+        nat.check(L_.lgm_mva_norm_tokens_backward(_dtype_code(x), _dtype_code(d_tok), B, F, C, H * W, groups,
+                                                  nat.ptr(x), nat.ptr(gamma), nat.ptr(mean), nat.ptr(rstd),
+                                                  nat.ptr(d_tok), nat.ptr(d_res), nat.ptr(dx), nat.ptr(dw),
+                                                  nat.ptr(db), nat.ptr(ws), ws_bytes, nat.stream_of(x.device),
+                                                  nat.diag()), "lgm_mva_norm_tokens_backward")
         dw = None if dw is None else dw.to(weight.dtype)
         db = None if db is None else db.to(weight.dtype)
         return dx, dw, db, None, None, None, None
@@ -188,7 +204,8 @@ class _NormTokens(torch.autograd.Function):
 
 class _TokensOut(torch.autograd.Function):
     """MVAttention's [B, F*H*W, C] -> [B*F, C, H, W] permute fused with (y + res) * skip_scale (core/unet.py:45-48),
-    one HIP pass (lgm_mva_tokens_out); res None: the permute alone."""
+    one HIP pass (lgm_mva_tokens_out); res None: the permute alone. Backward: one HIP pass
+    (lgm_mva_tokens_out_backward) writes the tokens' gradient and the residual's."""
 
     @staticmethod
     def forward(ctx, y, res, F: int, H: int, W: int, skip: float):
@@ -206,9 +223,15 @@ class _TokensOut(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_out):
         B, F, C, H, W, skip, ydt, rdt = ctx.meta
-        g = d_out if rdt is None else d_out * skip
-        d_y = g.reshape(B, F, C, H, W).permute(0, 1, 3, 4, 2).reshape(B, F * H * W, C).to(ydt)
-        d_res = None if rdt is None else g.to(rdt)
+        d_out = d_out.contiguous()
+        d_y = torch.empty((B, F * H * W, C), device=d_out.device, dtype=ydt)
+        want_res = rdt is not None and ctx.needs_input_grad[1]
+        d_res = torch.empty((B * F, C, H, W), device=d_out.device, dtype=rdt) if want_res else None
+        nat.check(nat.lib().lgm_mva_tokens_out_backward(_dtype_code(d_out), _dtype_code(d_y),
+                                                        _dtype_code(d_res) if want_res else 0, B, F, C, H * W,
+                                                        nat.ptr(d_out), skip if rdt is not None else 1.0,
+                                                        nat.ptr(d_y), nat.ptr(d_res), nat.stream_of(d_out.device),
+                                                        nat.diag()), "lgm_mva_tokens_out_backward")
         return d_y, d_res, None, None, None, None
 
 
@@ -238,10 +261,10 @@ class MVAttention(nn.Module):
             # fused token layout kernels around the attention core (same math; GroupNorm in fp32 as under autocast)
             ac = _autocast_dtype("cuda")
             tok_dtype = ac if ac is not None else x.dtype
-            tok = _NormTokens.apply(x, self.norm.weight, self.norm.bias, self.num_frames, self.norm.num_groups,
-                                    self.norm.eps, tok_dtype)
+            tok, xres = _NormTokens.apply(x, self.norm.weight, self.norm.bias, self.num_frames, self.norm.num_groups,
+                                          self.norm.eps, tok_dtype)
             y = self.attn(tok)
-            return _TokensOut.apply(y, x if self.residual else None, self.num_frames, H, W,
+            return _TokensOut.apply(y, xres if self.residual else None, self.num_frames, H, W,
                                     self.skip_scale if self.residual else 1.0)
         res = x
         x = self.norm(x)

@@ -176,6 +176,202 @@ __global__ __launch_bounds__(256) void k_mva_out(int F, int C, int HW, const TY 
     }
 }
 
+// ---- backward (core/unet.py:40-48 backward), the mirror of the two passes above:
+// k_mva_out_bwd   grid (ceil(HW/64), ceil(C/64), B*F): g = dL/dout * scale (rounded to out's dtype, as torch's
+//                 `d_out * skip`), written to d_res [B*F, C, H, W] along hw and, through the 64 x 64 LDS tile, to the
+//                 tokens' gradient d_y [B, F*H*W, C] along c.
+// k_mva_gn_part   grid (ceil(HW/64), ceil(C/64), B*F): per (sample, channel, 64-pixel tile) partial sums of
+//                 dy * x and dy (dy = the token gradient read back through the LDS tile) -> part2
+// k_mva_gn_coef   grid (G): per (sample, channel) ds = sum dy x, db = sum dy (fixed order over the tiles), then per
+//                 (sample, group) torch's fused backward parameters c2, c3 and per channel dgamma, dbeta (fixed
+//                 order over the samples): deterministic
+// k_mva_gn_dx     grid (ceil(HW/64), ceil(C/64), B*F): dx = rstd gamma dy + c2 x + c3 (+ d_res), one rounding to
+//                 x's dtype: the GroupNorm backward and autograd's sum with the residual's gradient in one pass.
+template <class TD, class TY, class TR>
+__global__ __launch_bounds__(256) void k_mva_out_bwd(int F, int C, int HW, const TD *__restrict__ dout, float scale,
+                                                     TY *__restrict__ dy, TR *__restrict__ dres) {
+    __shared__ float tile[64][65];  // [channel][pixel]
+    const int hw0 = blockIdx.x * 64, c0 = blockIdx.y * 64, bf = blockIdx.z, tid = threadIdx.x;
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {  // all loads in flight before the first use (clamped, unconditional addresses)
+        const int i = tid + 256 * k, r = i >> 6, h = i & 63;  // channel r, pixel h
+        const bool ok = hw0 + h < HW && c0 + r < C;
+        v[k] = to_f(dout[ok ? ((size_t)bf * C + c0 + r) * HW + hw0 + h : 0]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int i = tid + 256 * k, r = i >> 6, h = i & 63;
+        const float g = to_f(from_f<TD>(v[k] * scale));  // (exact: scale 1 and an fp32 gradient)
+        tile[r][h] = g;
+        if (dres && hw0 + h < HW && c0 + r < C) dres[((size_t)bf * C + c0 + r) * HW + hw0 + h] = from_f<TR>(g);
+    }
+    __syncthreads();
+    const int b = bf / F, f = bf - b * F;
+    TY *yb = dy + ((size_t)b * F * HW + (size_t)f * HW) * C;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int i = tid + 256 * k, r = i >> 6, c = i & 63;  // token row r, channel c
+        if (hw0 + r < HW && c0 + c < C) yb[(size_t)(hw0 + r) * C + c0 + c] = from_f<TY>(tile[c][r]);
+    }
+}
+
+// the token gradient of a 64-channel x 64-pixel tile into LDS as [pixel][channel] (reads along c), zero outside
+template <class TT>
+__device__ __forceinline__ void load_tok_tile(float (&tile)[64][65], const TT *__restrict__ tok, int F, int C, int HW,
+                                              int bf, int hw0, int c0) {
+    const int b = bf / F, f = bf - b * F, tid = threadIdx.x;
+    const TT *tb = tok + ((size_t)b * F * HW + (size_t)f * HW) * C;
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int i = tid + 256 * k, r = i >> 6, c = i & 63;  // token row r, channel c
+        const bool ok = hw0 + r < HW && c0 + c < C;
+        v[k] = to_f(tb[ok ? (size_t)(hw0 + r) * C + c0 + c : 0]);
+        v[k] = ok ? v[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int i = tid + 256 * k, r = i >> 6, c = i & 63;
+        tile[r][c] = v[k];
+    }
+}
+
+template <class TI, class TT>
+__global__ __launch_bounds__(256) void k_mva_gn_part(int F, int C, int HW, const TI *__restrict__ x,
+                                                     const TT *__restrict__ dtok, float2 *__restrict__ part) {
+    __shared__ float tile[64][65];  // dy [pixel][channel]
+    __shared__ float xs[64][65];    // x [channel][pixel]
+    __shared__ float2 red[4][64];
+    const int hw0 = blockIdx.x * 64, c0 = blockIdx.y * 64, bf = blockIdx.z, tid = threadIdx.x;
+    const int nT = gridDim.x;
+    {
+        float xv[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {  // x along hw (zero outside), issued before the token tile's loads
+            const int i = tid + 256 * k, r = i >> 6, h = i & 63;  // channel r, pixel h
+            const bool ok = hw0 + h < HW && c0 + r < C;
+            xv[k] = to_f(x[ok ? ((size_t)bf * C + c0 + r) * HW + hw0 + h : 0]);
+            xv[k] = ok ? xv[k] : 0.f;
+        }
+        load_tok_tile(tile, dtok, F, C, HW, bf, hw0, c0);
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int i = tid + 256 * k, r = i >> 6, h = i & 63;
+            xs[r][h] = xv[k];
+        }
+    }
+    __syncthreads();
+    // thread: channel c = tid & 63, pixels 16 q .. 16 q + 15 (q = the wave); the four quarters summed in order
+    const int c = tid & 63, q = tid >> 6;
+    float sdx = 0.f, sd = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int h = 16 * q + k;
+        const float g = tile[h][c];
+        sd += g;
+        sdx = fmaf(g, xs[c][h], sdx);
+    }
+    red[q][c] = make_float2(sdx, sd);
+    __syncthreads();
+    if (tid < 64 && c0 + tid < C) {
+        const float2 a = red[0][tid], b2 = red[1][tid], c2 = red[2][tid], d2 = red[3][tid];
+        part[((size_t)bf * C + c0 + tid) * nT + blockIdx.x] =
+            make_float2((a.x + b2.x) + (c2.x + d2.x), (a.y + b2.y) + (c2.y + d2.y));
+    }
+}
+
+constexpr int GN_NMAX = 2048;  // (sample, channel) pairs of one group held in LDS at a time
+__global__ __launch_bounds__(256) void k_mva_gn_coef(int BF, int C, int HW, int G, int nT,
+                                                     const float2 *__restrict__ part, const float *__restrict__ gamma,
+                                                     const float *__restrict__ mean, const float *__restrict__ rstd,
+                                                     float2 *__restrict__ coef, float *__restrict__ dgamma,
+                                                     float *__restrict__ dbeta) {
+    __shared__ float2 sdb[GN_NMAX];  // (ds, db) of the chunk's (sample, channel) pairs
+    const int g = blockIdx.x, Cg = C / G, tid = threadIdx.x;
+    const float s = 1.f / ((float)Cg * (float)HW);
+    const int nchunk = max(1, GN_NMAX / Cg);  // samples per LDS chunk
+    float dg = 0.f, dbt = 0.f;                // this thread's channel (tid < Cg), summed over the samples in order
+    for (int n0 = 0; n0 < BF; n0 += nchunk) {
+        const int n1 = min(BF, n0 + nchunk), items = (n1 - n0) * Cg;
+        for (int it = tid; it < items; it += 256) {
+            const int n = n0 + it / Cg, c = g * Cg + it % Cg;
+            const float2 *pp = part + ((size_t)n * C + c) * nT;
+            float a = 0.f, b = 0.f;
+            for (int t = 0; t < nT; t++) {  // fixed order over the pixel tiles
+                const float2 p = pp[t];
+                a += p.x;
+                b += p.y;
+            }
+            sdb[it] = make_float2(a, b);
+        }
+        __syncthreads();
+        for (int n = n0 + tid; n < n1; n += 256) {  // per sample: torch's fused backward parameters
+            float sum1 = 0.f, sum2 = 0.f;
+            for (int cc = 0; cc < Cg; cc++) {
+                const float ga = gamma ? gamma[g * Cg + cc] : 1.f;
+                const float2 v = sdb[(n - n0) * Cg + cc];
+                sum1 = fmaf(v.x, ga, sum1);
+                sum2 = fmaf(v.y, ga, sum2);
+            }
+            const float mu = mean[(size_t)n * G + g], rs = rstd[(size_t)n * G + g];
+            const float c2 = (sum2 * mu - sum1) * rs * rs * rs * s;
+            const float c3 = -c2 * mu - sum2 * rs * s;
+            coef[(size_t)n * G + g] = make_float2(c2, c3);
+        }
+        if (tid < Cg) {  // per channel: dgamma, dbeta over this chunk's samples, in order
+            for (int n = n0; n < n1; n++) {
+                const float2 v = sdb[(n - n0) * Cg + tid];
+                const float mu = mean[(size_t)n * G + g], rs = rstd[(size_t)n * G + g];
+                dg = fmaf(v.x - v.y * mu, rs, dg);
+                dbt += v.y;
+            }
+        }
+        __syncthreads();  // (sdb is rewritten by the next chunk)
+    }
+    if (tid < Cg) {
+        if (dgamma) dgamma[g * Cg + tid] = dg;
+        if (dbeta) dbeta[g * Cg + tid] = dbt;
+    }
+}
+
+template <class TI, class TT, class TR>
+__global__ __launch_bounds__(256) void k_mva_gn_dx(int F, int C, int HW, int G, const TI *__restrict__ x,
+                                                   const TT *__restrict__ dtok, const TR *__restrict__ dres,
+                                                   const float *__restrict__ gamma, const float *__restrict__ rstd,
+                                                   const float2 *__restrict__ coef, TI *__restrict__ dx) {
+    __shared__ float tile[64][65];  // [pixel][channel]
+    __shared__ float sa[64], sb[64], sc[64];
+    const int hw0 = blockIdx.x * 64, c0 = blockIdx.y * 64, bf = blockIdx.z, tid = threadIdx.x;
+    const int Cg = C / G;
+    if (tid < 64 && c0 + tid < C) {
+        const int c = c0 + tid, g = c / Cg;
+        const float2 k = coef[(size_t)bf * G + g];
+        sa[tid] = rstd[(size_t)bf * G + g] * (gamma ? gamma[c] : 1.f);
+        sb[tid] = k.x;
+        sc[tid] = k.y;
+    }
+    load_tok_tile(tile, dtok, F, C, HW, bf, hw0, c0);
+    float xv[16], rv[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {  // x and the residual's gradient along hw, all in flight before the barrier
+        const int i = tid + 256 * k, r = i >> 6, h = i & 63;  // channel r, pixel h
+        const bool ok = hw0 + h < HW && c0 + r < C;
+        const size_t o = ok ? ((size_t)bf * C + c0 + r) * HW + hw0 + h : 0;
+        xv[k] = to_f(x[o]);
+        rv[k] = dres ? to_f(dres[o]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int i = tid + 256 * k, r = i >> 6, h = i & 63;
+        if (hw0 + h < HW && c0 + r < C) {
+            const float v = fmaf(sa[r], tile[h][r], fmaf(sb[r], xv[k], sc[r])) + rv[k];
+            dx[((size_t)bf * C + c0 + r) * HW + hw0 + h] = from_f<TI>(v);
+        }
+    }
+}
+
 template <class TI, class TO>
 int launch_norm(int B, int F, int C, int HW, int G, float eps, const void *x, const float *gamma, const float *beta,
                 void *tok, float *mean, float *rstd, float2 *part, hipStream_t st) {
@@ -232,8 +428,100 @@ int out_by_r(int dtr, int dto, int B, int F, int C, int HW, const void *y, const
     return LGM_E_INVALID;
 }
 
+// backward launchers: the dtype switches (LGM_ATTN_F32 / BF16 / F16 codes -> types)
+template <class Fn>
+int with_type(int code, Fn &&fn) {
+    switch (code) {
+        case LGM_ATTN_F32: return fn(float{});
+        case LGM_ATTN_BF16: return fn(__hip_bfloat16{});
+        case LGM_ATTN_F16: return fn(__half{});
+    }
+    set_error("lgm_mva backward: bad dtype %d", code);
+    return LGM_E_INVALID;
+}
+
+size_t gn_part_bytes(int BF, int C, int HW) { return (((size_t)BF * C * ((HW + 63) / 64) * sizeof(float2)) + 255) & ~(size_t)255; }
+
 }  // namespace
 }  // namespace lgm
+
+extern "C" size_t lgm_mva_backward_workspace_size(int B, int F, int C, int HW, int groups) {
+    if (B <= 0 || F <= 0 || C <= 0 || HW <= 0 || groups <= 0 || C % groups) return 0;
+    return lgm::gn_part_bytes(B * F, C, HW) + (size_t)B * F * groups * sizeof(float2);
+}
+
+extern "C" int lgm_mva_tokens_out_backward(int dtype_dout, int dtype_dy, int dtype_dres, int B, int F, int C, int HW,
+                                           const void *d_out, float scale, void *d_y, void *d_res, void *stream,
+                                           const lgm_diag *diag) {
+    lgm::clear_error();
+    lgm::DiagScope ds(diag);
+    if (B < 0 || F <= 0 || C <= 0 || HW < 0) {
+        lgm::set_error("lgm_mva_tokens_out_backward: bad shape B=%d F=%d C=%d HW=%d", B, F, C, HW);
+        return LGM_E_INVALID;
+    }
+    if (B == 0 || HW == 0) return LGM_OK;
+    if (!d_out || !d_y) {
+        lgm::set_error("lgm_mva_tokens_out_backward: null pointer");
+        return LGM_E_INVALID;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((HW + 63) / 64, (C + 63) / 64, B * F);
+    return lgm::with_type(dtype_dout, [&](auto td) {
+        using TD = decltype(td);
+        return lgm::with_type(dtype_dy, [&](auto ty) {
+            using TY = decltype(ty);
+            return lgm::with_type(d_res ? dtype_dres : LGM_ATTN_F32, [&](auto tr) {
+                using TR = decltype(tr);
+                LGM_LAUNCH("k_mva_out_bwd", st, (lgm::k_mva_out_bwd<TD, TY, TR><<<grid, 256, 0, st>>>(
+                                                     F, C, HW, (const TD *)d_out, scale, (TY *)d_y, (TR *)d_res)));
+                return LGM_OK;
+            });
+        });
+    });
+}
+
+extern "C" int lgm_mva_norm_tokens_backward(int dtype_x, int dtype_tok, int B, int F, int C, int HW, int groups,
+                                            const void *x, const float *gamma, const float *mean, const float *rstd,
+                                            const void *d_tokens, const void *d_res, void *dx, float *dgamma,
+                                            float *dbeta, void *workspace, size_t workspace_bytes, void *stream,
+                                            const lgm_diag *diag) {
+    lgm::clear_error();
+    lgm::DiagScope ds(diag);
+    if (B < 0 || F <= 0 || C <= 0 || HW < 0 || groups <= 0 || C % groups || C / groups > 256) {
+        lgm::set_error("lgm_mva_norm_tokens_backward: bad shape B=%d F=%d C=%d HW=%d groups=%d (channels per group "
+                       "<= 256)", B, F, C, HW, groups);
+        return LGM_E_INVALID;
+    }
+    if (B == 0 || HW == 0) return LGM_OK;
+    if (!x || !mean || !rstd || !d_tokens || !workspace) {
+        lgm::set_error("lgm_mva_norm_tokens_backward: null pointer");
+        return LGM_E_INVALID;
+    }
+    if (workspace_bytes < lgm_mva_backward_workspace_size(B, F, C, HW, groups)) {
+        lgm::set_error("lgm_mva_norm_tokens_backward: workspace too small");
+        return LGM_E_WORKSPACE;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const int BF = B * F, nT = (HW + 63) / 64;
+    float2 *part = (float2 *)workspace;
+    float2 *coef = (float2 *)((char *)workspace + lgm::gn_part_bytes(BF, C, HW));
+    const dim3 grid(nT, (C + 63) / 64, BF);
+    return lgm::with_type(dtype_x, [&](auto tx) {
+        using TI = decltype(tx);
+        return lgm::with_type(dtype_tok, [&](auto tt) {
+            using TT = decltype(tt);
+            LGM_LAUNCH("k_mva_gn_part", st, (lgm::k_mva_gn_part<TI, TT><<<grid, 256, 0, st>>>(
+                                                 F, C, HW, (const TI *)x, (const TT *)d_tokens, part)));
+            LGM_LAUNCH("k_mva_gn_coef", st, (lgm::k_mva_gn_coef<<<groups, 256, 0, st>>>(
+                                                 BF, C, HW, groups, nT, part, gamma, mean, rstd, coef, dgamma, dbeta)));
+            if (dx)
+                LGM_LAUNCH("k_mva_gn_dx", st, (lgm::k_mva_gn_dx<TI, TT, TI><<<grid, 256, 0, st>>>(
+                                                   F, C, HW, groups, (const TI *)x, (const TT *)d_tokens,
+                                                   (const TI *)d_res, gamma, rstd, coef, (TI *)dx)));
+            return LGM_OK;
+        });
+    });
+}
 
 extern "C" size_t lgm_mva_workspace_size(int B, int F, int C, int HW, int groups) {
     if (B <= 0 || F <= 0 || C <= 0 || HW <= 0 || groups <= 0 || C % groups) return 0;

@@ -31,8 +31,10 @@ extern "C" {
 #define LGM_ATTN_BF16 1
 #define LGM_ATTN_F16 2
 
-/* Bytes of device scratch lgm_attn_backward needs (the fp32 delta = rowsum(dO * O) buffer). */
-size_t lgm_attn_workspace_size(int dtype, int B, int L, int H);
+/* Bytes of device scratch lgm_attn_backward needs: the fp32 delta = rowsum(dO * O) buffer, and for 16-bit dtypes
+ * the rounded Q * scale * log2(e) rows the dQ pass hands to the dK/dV pass (both recompute the forward's P from the
+ * same rounded operands). */
+size_t lgm_attn_workspace_size(int dtype, int B, int L, int H, int D);
 
 /* o = softmax(scale * q k^T) v per (batch, head); also writes lse. */
 int lgm_attn_forward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,

@@ -26,7 +26,7 @@ extern "C" {
 const char *lgm_last_error(void);
 
 /* ABI version (bumped on any signature change). 3: per-call lgm_diag, LGM_RENDER_NO_CULL as a per-call option.
- * 4: lgm_diag.det_limit_log2. */
+ * 4: lgm_diag.det_limit_log2. 5: lgm_attn_workspace_size takes D. */
 int lgm_abi_version(void);
 
 /* Profiler object: create, read per-kernel totals, reset, destroy. It records into itself only while a call is

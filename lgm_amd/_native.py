@@ -36,7 +36,7 @@ SIGNATURES = {
                                   _vp, _vp]),
     "lgm_attn_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp, _c_ll, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _c_ll, _vp, _c_size, _vp, _vp]),
-    "lgm_attn_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "lgm_attn_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "lgm_mva_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "lgm_mva_norm_tokens": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp,
                                      _vp, _vp, _vp, _vp, _c_size, _vp, _vp]),
@@ -72,7 +72,7 @@ SIGNATURES = {
 _lib = None
 
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 RENDER_NO_CULL = 1  # include/lgm_render.h LGM_RENDER_NO_CULL
 RENDER_CLAMP_IMAGE = 2  # include/lgm_render.h LGM_RENDER_CLAMP_IMAGE
 RENDER_BACKWARD_AGAIN = 4  # include/lgm_render.h LGM_RENDER_BACKWARD_AGAIN

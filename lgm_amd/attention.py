@@ -61,7 +61,7 @@ class _PackedAttention(torch.autograd.Function):
         if B * L * H > 0:
             dt = _dtype_code(qkv)
             L_ = nat.lib()
-            ws_bytes = L_.lgm_attn_workspace_size(dt, B, L, H)
+            ws_bytes = L_.lgm_attn_workspace_size(dt, B, L, H, D)
             ws = torch.empty(max(ws_bytes, 1), device=qkv.device, dtype=torch.uint8)
             base, dbase, es = qkv.data_ptr(), d_qkv.data_ptr(), qkv.element_size()
             hd = H * D * es

@@ -648,23 +648,11 @@ struct TileLoader {  // one 64-row tile of up to two [tokens][ld] tensors, CH 16
             *reinterpret_cast<uint4 *>(tb + r * ldt + col) = b[cc];
         }
     }
-    // a second image of the first tensor, each element times c rounded to T (as prescale() rounds a register operand)
-    __device__ __forceinline__ void store_scaled_a(T *tc, int ldt, float c) {
-#pragma unroll
-        for (int cc = 0; cc < CH; cc++) {
-            const int ci = threadIdx.x + cc * NT, r = ci / (D / 8), col = (ci - r * (D / 8)) * 8;
-            const T *e = reinterpret_cast<const T *>(&a[cc]);
-            T o[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) o[j] = (T)((float)e[j] * c);
-            *reinterpret_cast<uint4 *>(tc + r * ldt + col) = *reinterpret_cast<const uint4 *>(o);
-        }
-    }
 };
 
 // dK, dV: grid (ceil(L / (64 KS)), B*H); wavefront w owns keys k0 + 16 s + (lane & 15), s < KS.
 template <int DT, int D, int KS>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DKDV_WPE32 : D <= 64 ? BWD_WPE : 1))) void k_attn_dkdv2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DKDV_WPE32 : D <= 64 ? BWD_WPE : 1))) void k_attn_dkdv2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ qc,
                                                    const typename Ty<DT>::T *__restrict__ k,
                                                    const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                    const typename Ty<DT>::T *__restrict__ dout,
@@ -674,8 +662,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
     constexpr int LDK = D + LDK_PAD;
-    __shared__ __attribute__((aligned(16))) T Qs[2][64 * LDK];
-    __shared__ __attribute__((aligned(16))) T Qc[2][64 * LDK];  // Q * scale * log2(e), rounded: the S operand
+    __shared__ __attribute__((aligned(16))) T Qs[2][64 * LDK];  // Q * scale * log2(e), rounded (k_attn_dq2's qc)
     __shared__ __attribute__((aligned(16))) T Os[2][64 * LDK];
     __shared__ float sl[2][64], sd[2][64];
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -683,16 +670,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     const long long obase = (long long)b * L * H * D + (long long)h * D;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
     const int k0 = blockIdx.x * (64 * KS) + w * (16 * KS);
-    const float c = scale * LOG2E;
+    const float dk_scale = 1.0f / LOG2E;  // scale / c: dK = scale sum dS^T Q = (scale / c) sum dS^T (Q c)
     YFrag<DT, D> kf[KS], vf[KS];
 #pragma unroll
     for (int s = 0; s < KS; s++) {
         const int kr = k0 + 16 * s + r16;
         load_yfrag<DT, D>(kf[s], k + base + (long long)kr * ld, kr < L, g);
         load_yfrag<DT, D>(vf[s], v + base + (long long)kr * ld, kr < L, g);
-#ifdef LGM_AB_KPRE
-        prescale<DT, D / 32>(kf[s].v, c);
-#endif
     }
     f32x4 dka[KS][D / 16], dva[KS][D / 16];
 #pragma unroll
@@ -702,7 +686,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     TileLoader<T, D> ld_;
     float pl = 0.f, pd = 0.f;
     auto load_rows2 = [&](int qb) {
-        ld_.load(q + base, ld, dout + obase, (long long)H * D, qb, L);
+        ld_.load(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L);
         if (tid < 64) {
             const bool qv = qb + tid < L;
             pl = qv ? lse[(long long)bh * L + qb + tid] * LOG2E : INFINITY;  // invalid rows: P = 0
@@ -710,12 +694,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
         }
     };
     auto store_rows2 = [&](int buf) {
+        // S from the same rounded operand as k_attn_fwd2 / k_attn_dq2 (Q * c, which k_attn_dq2 wrote; K unscaled),
+        // so the P recomputed here is the P whose row sums gave lse (with K * c instead, dK / dV were 1.8x further from
+        // fp64: 7.2e-3 vs 4.0e-3 rel L2, bf16 at L 4096; profiles/r05/attn_prescale). dK's product reads the same
+        // image and is rescaled by scale / c at the end (a second, unscaled Q image cost +15 % dK,dV time; scaling
+        // the staged tile here +8.5 %)
         ld_.store(Qs[buf], Os[buf], LDK);
-        // S from the same rounded operand as k_attn_fwd2 / k_attn_dq2 (Q * c; K unscaled), so the P recomputed here
-        // is the P whose row sums gave lse; dK's product keeps the unscaled image
-#ifndef LGM_AB_KPRE
-        ld_.store_scaled_a(Qc[buf], LDK, c);
-#endif
         if (tid < 64) {  // stored negated: the accumulator inits
             // (the row index recomputed here: the two LDS addresses hoisted out of the query loop were spilled at the
             // 128-VGPR cap, and their scratch reloads sat on wave 0's path to every tile's barrier)
@@ -732,7 +716,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     for (int qb = 0; qb < L; qb += 64) {
         const bool more = qb + 64 < L;
         if (more) load_rows2(qb + 64);
-        const T *Qt = Qs[cur], *Qct = Qc[cur], *Ot = Os[cur];
+        const T *Qt = Qs[cur], *Ot = Os[cur];  // (dK from Q * c: rescaled below)
         // the tile's two 32-query halves one after the other (S / dP of subs 2t, 2t + 1, then their dV / dK
         // products): half the score registers live at once (dK,dV at D = 32 fits 4 waves per SIMD instead of 3)
 #pragma unroll
@@ -744,11 +728,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
                 V8 qr[D / 32], orr[D / 32];
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
-#ifdef LGM_AB_KPRE
                     qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
-#else
-                    qr[cc] = *reinterpret_cast<const V8 *>(Qct + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
-#endif
                     orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
                 }
                 // (the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i, read as stored)
@@ -806,7 +786,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
             for (int dt = 0; dt < D / 16; dt++)
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    krow[16 * dt + 4 * g + i] = from_f<T>(dka[s][dt][i] * scale);
+                    krow[16 * dt + 4 * g + i] = from_f<T>(dka[s][dt][i] * dk_scale);
                     vrow[16 * dt + 4 * g + i] = from_f<T>(dva[s][dt][i]);
                 }
         }
@@ -821,7 +801,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                                                  const typename Ty<DT>::T *__restrict__ dout,
                                                  const float *__restrict__ lse, float *__restrict__ delta,
                                                  typename Ty<DT>::T *__restrict__ dq, long long ldd,
-                                                 const typename Ty<DT>::T *__restrict__ o) {
+                                                 const typename Ty<DT>::T *__restrict__ o,
+                                                 typename Ty<DT>::T *__restrict__ qc) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
     constexpr int LDK = D + LDK_PAD;
@@ -859,6 +840,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
             if (qv && g == 0) delta[(long long)bh * L + qr] = part;
         }
         prescale<DT, D / 32>(qf[s].v, c);  // S in log2 units
+        if (qv) {  // the rounded Q * c rows for k_attn_dkdv2 ([B*H][L][D]), so it recomputes this P exactly
+            T *dst = qc + ((long long)bh * L + qr) * D;
+#pragma unroll
+            for (int cc = 0; cc < D / 32; cc++) *reinterpret_cast<V8 *>(dst + 32 * cc + 8 * g) = qf[s].v[cc];
+        }
     }
     f32x4 dqa[QS][D / 16];
 #pragma unroll
@@ -967,25 +953,29 @@ int fwd_impl(int B, int L, int H, float scale, const void *q, const void *k, con
     return LGM_OK;
 }
 
+// backward workspace: delta [B*H][L] fp32, then (16-bit types) Q * scale * log2(e) [B*H][L][D] in the input type
+size_t qc_offset(int B, int L, int H) { return ((size_t)B * L * H * sizeof(float) + 255) & ~(size_t)255; }
+
 template <int DT, int D>
 int bwd_impl(int B, int L, int H, float scale, const void *q, const void *k, const void *v, long long ld,
              const void *o, const float *lse, const void *dout, void *dq, void *dk, void *dv, long long ldd,
              float *delta, hipStream_t st) {
     using T = typename Ty<DT>::T;
     const long long rows = (long long)B * L * H;
+    T *qc = reinterpret_cast<T *>(reinterpret_cast<char *>(delta) + qc_offset(B, L, H));  // (16-bit paths)
     if constexpr (DT != LGM_ATTN_F32) {  // (delta computed by k_attn_dq2 itself)
         constexpr int S2 = D <= 32 ? 2 : 1;  // two 16-row sub-tiles per wavefront where registers allow
         const bool two = S2 == 2 && (long long)((L + 127) / 128) * B * H >= 512;
         dim3 g2((L + (two ? 127 : 63)) / (two ? 128 : 64), B * H);
         if (two) {
             LGM_LAUNCH("k_attn_dq", st, (k_attn_dq2<DT, D, S2><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
-                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd, (const T *)o)));
-            LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, S2><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
+                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd, (const T *)o, qc)));
+            LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, S2><<<g2, NT, 0, st>>>(L, H, scale, (const T *)qc,
                        (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dk, (T *)dv, ldd)));
         } else {
             LGM_LAUNCH("k_attn_dq", st, (k_attn_dq2<DT, D, 1><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
-                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd, (const T *)o)));
-            LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, 1><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
+                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd, (const T *)o, qc)));
+            LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, 1><<<g2, NT, 0, st>>>(L, H, scale, (const T *)qc,
                        (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dk, (T *)dv, ldd)));
         }
         return LGM_OK;
@@ -1030,9 +1020,10 @@ int check(int dtype, int B, int L, int H, int D) {
 
 extern "C" {
 
-size_t lgm_attn_workspace_size(int dtype, int B, int L, int H) {
-    if (B <= 0 || L <= 0 || H <= 0) return 0;
-    return (size_t)B * L * H * sizeof(float);  // delta
+size_t lgm_attn_workspace_size(int dtype, int B, int L, int H, int D) {
+    if (B <= 0 || L <= 0 || H <= 0 || D <= 0) return 0;
+    if (dtype == LGM_ATTN_F32) return (size_t)B * L * H * sizeof(float);  // delta
+    return lgm::attn::qc_offset(B, L, H) + (size_t)B * L * H * D * 2;      // delta, Q * c
 }
 
 int lgm_attn_forward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,
@@ -1061,7 +1052,7 @@ int lgm_attn_backward(int dtype, int B, int L, int H, int D, float scale, const 
         lgm::set_error("null pointer");
         return LGM_E_INVALID;
     }
-    if (!workspace || workspace_bytes < lgm_attn_workspace_size(dtype, B, L, H)) {
+    if (!workspace || workspace_bytes < lgm_attn_workspace_size(dtype, B, L, H, D)) {
         lgm::set_error("attention workspace too small");
         return LGM_E_WORKSPACE;
     }

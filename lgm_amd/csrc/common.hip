@@ -77,7 +77,7 @@ void prof_end(hipStream_t st) {
 
 extern "C" {
 const char *lgm_last_error(void) { return lgm::g_err; }
-int lgm_abi_version(void) { return 4; }
+int lgm_abi_version(void) { return 5; }
 
 lgm_profiler *lgm_profiler_create(void) { return new lgm_profiler(); }
 int lgm_profiler_reset(lgm_profiler *p) {

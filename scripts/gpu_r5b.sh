@@ -20,4 +20,10 @@ for l in open('gpurun_out/r5b/attn_${n}_r${round}.jsonl'):
   done
 done
 timeout -k 10 600 python -u -m pytest -x -v -s --timeout 240 --timeout-method thread tests/test_render_gpu.py tests/test_head.py -m gpu -k "needle or saturation or retain or head" > gpurun_out/r5b/t_render_new.log 2>&1
-rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/r5b/t_render_new.log | tail -30; grep "^head " gpurun_out/r5b/t_render_new.log | head -60; exit $rc
+rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/r5b/t_render_new.log | tail -30; grep "^head " gpurun_out/r5b/t_render_new.log | head -60; [ $rc -eq 0 ] || exit $rc
+# backward section shares (LGM_BWD_STAMPS build) on the pool and one scene, and the single scene's work timelines
+LGM_AMD_LIB=$PWD/lgm_amd/_lib/variants/lib_stamps.so timeout -k 10 200 python scripts/diag_bwd_stamps.py 8 > gpurun_out/r5b/stamps_B8.json 2>&1 || exit $?
+LGM_AMD_LIB=$PWD/lgm_amd/_lib/variants/lib_stamps.so timeout -k 10 200 python scripts/diag_bwd_stamps.py 1 > gpurun_out/r5b/stamps_B1.json 2>&1 || exit $?
+tail -1 gpurun_out/r5b/stamps_B8.json; tail -1 gpurun_out/r5b/stamps_B1.json
+timeout -k 10 200 python scripts/diag_counters.py 1 > gpurun_out/r5b/counters_B1.log 2>&1 || exit $?
+tail -5 gpurun_out/r5b/counters_B1.log | cut -c1-600

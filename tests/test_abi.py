@@ -43,7 +43,8 @@ def test_workspace_and_errors():
     # attention: unsupported head dim / dtype are reported, never thrown
     rc = L.lgm_attn_forward(1, 1, 16, 2, 48, 0.1, None, None, None, 0, None, None, None, None)
     assert rc < 0 and b"D must be" in L.lgm_last_error()
-    assert L.lgm_attn_workspace_size(1, 2, 100, 4) == 2 * 100 * 4 * 4
+    assert L.lgm_attn_workspace_size(0, 2, 100, 4, 32) == 2 * 100 * 4 * 4  # fp32: delta
+    assert L.lgm_attn_workspace_size(1, 2, 100, 4, 32) >= 2 * 100 * 4 * (4 + 2 * 32)  # bf16: delta + Q * c
 
 
 def test_no_process_wide_switches():

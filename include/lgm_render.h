@@ -120,7 +120,7 @@ int lgm_render_records(int B, int V, int N, int H, int W, const void *workspace,
 int lgm_render_needle_flags(long long n, const float *abc, unsigned char *flags_out, void *stream);
 
 /* Diagnostics: when diag->render_counters (a DEVICE uint64 buffer, caller-zeroed) is set, that call's render kernels
- * record per-workgroup timelines in it: [0..7] section cycles of the LGM_BWD_STAMPS diagnostic build (else unused);
+ * record per-workgroup timelines in it: [0..7] the backward's section cycles in the LGM_BWD_STAMPS diagnostic build (else unused);
  * then 8 entries per tile t (B*V*T tiles): s_memrealtime stamps (100 MHz) [8+8t] fwd start, [+1] fwd end,
  * [+2], [+3] the start / end of preprocess-backward workgroup t (t < its grid), [+4] sort start, [+5] sort end,
  * [+6] the tile's binned list length (low 32 bits; k_sort writes it, k_render_fwd rewrites it with the HW_ID of the

@@ -62,11 +62,6 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
 typedef __attribute__((ext_vector_type(2))) float f32x2v;
 constexpr int MB = 8;      // entries per moment-MFMA batch (columns 0..7: w, 8..15: u)
-#ifdef LGM_BWD_WAVEFLUSH
-constexpr bool kWaveFlush = true;
-#else
-constexpr bool kWaveFlush = false;
-#endif
 
 // One staged 256-entry chunk, written by LDS DMA (global_load_lds: 16-B lane stride for both the 16-B and the
 // 12-B form): P from gP, Q from gQ, R.xyz from the Gaussian row's colour; R.w holds the Gaussian id (written
@@ -697,7 +692,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     float *__restrict__ accum, const unsigned *__restrict__ det_max, unsigned *__restrict__ det_sat,
     long long item_stamps) {
     constexpr int NV = DEPTH ? NACC : NACC - 1;  // partials per (pixel, Gaussian): mean2D(2) conic(3) op rgb(3) [depth]
-    constexpr bool WF = kWaveFlush && !DET;      // per-wave conversion + flush (float mode; see the chunk loop)
     // entries per staged chunk; LDS row stride of the moment slots: LS = 4 (mod 32) puts the rows a moment store
     // writes at once (4 qk + rr, qk = 0, 1 in a 32-lane store group: rows rr and rr + 4) 16 banks apart, so a batch's
     // 8 consecutive entry columns land on distinct banks (ds_write_b32 banks are (a / 4) mod 32)
@@ -719,7 +713,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
     static_assert((NV + 3) * LS <= 16 * WU_LD, "the partial rows fit wave 0's WU image");
     __shared__ int s_ndl;  // the chunk holds a needle-like record (its conic partials go to the fp64 side block)
-    __shared__ unsigned s_ids[WF ? 2 : 1][WF ? CH : 1];  // wave-flush: the staged chunks' Gaussian ids
 
     // ---- work item: (tile, chunk c, checkpoint slot)
     const int M = d.BV * d.T, Mp = round8(M);  // head items, then the checkpoint items (none in deterministic mode)
@@ -754,9 +747,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const int s0e = c * TILE_PIX;
     unsigned id_cur = stager && s0e + tid < n ? ids[s0e + tid] : 0u;
     if (stager && s0e + tid < n) stage_dma(S.buf[0], w, id_cur, (size_t)bv * d.N, b, d.N, gP, gQ, gauss);
-    // (wave-flush: the chunk's ids in s_ids, written when the chunk is staged and published by the barrier that
-    // publishes the chunk -- not in R.w next to the DMA'd colour: the 12-B DMA's 16-B lane slot may land over it)
-    if (WF && stager) s_ids[0][tid] = id_cur;
     unsigned id_next = stager && s0e + BWD_CHUNK + tid < n ? ids[s0e + BWD_CHUNK + tid] : 0u;
     const size_t P = (size_t)d.H * d.W;
     const size_t pid = inside ? (size_t)d.W * py + px : 0;
@@ -800,8 +790,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         return;
     }
     const unsigned long long t_item = d.counters ? __builtin_amdgcn_s_memrealtime() : 0ull;
-#ifdef LGM_BWD_STAMPS  // section cycles of this wave (diagnostic build; counters [2..6], scripts/diag_bwd_stamps.py)
-    unsigned long long sec[5] = {0, 0, 0, 0, 0};
+#ifdef LGM_BWD_STAMPS  // section cycles of this wave (diagnostic build; counters [0..7], scripts/diag_bwd_stamps.py)
+    // [0] prologue, [1] chunk-top barrier, [2] chunk head (quadrant tests, compaction, next DMA issue), [3] entries
+    // loop, [4] the post-entries barrier + moments -> partials, [5] the DMA wait (vmcnt 0), [6] the pre-flush
+    // barrier, [7] the gradient atomics
+    unsigned long long sec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     SEC_T(ts_item);
 #endif
     const float bg_dot = bg[0] * dp0 + bg[1] * dp1 + bg[2] * dp2;
@@ -939,16 +932,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         SEC_T(ts_c0);
 #endif
         __syncthreads();
-        const int k = b0 + tid;
+#ifdef LGM_BWD_STAMPS
+        SEC_T(ts_c0b);
+        SEC_ADD(sec[1], ts_c0, ts_c0b);
+#endif
         auto &B = S.buf[cur];
+        const int k = b0 + tid;
         // one row per lane: every wave tests all CH entries against its OWN quadrant (one ellipse test per lane
         // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
-        if (!WF) {
-            if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
-            if (!DET && tid == 0) s_ndl = 0;  // (published by the barrier after the entries loop)
-            // every wave zeroes its own slot (an entry it skips, or never lists, adds nothing): wave-private, so the
-            // entries loop follows the quadrant tests without a barrier (with the conversion over three waves below:
-            // pool k_render_bwd 642 -> 635 us, bitwise equal, profiles/r04/ab_bwd_conv)
+        if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
+        if (!DET && tid == 0) s_ndl = 0;  // (published by the barrier after the entries loop)
+        {  // every wave zeroes its own slot (an entry it skips, or never lists, adds nothing): wave-private, so the
+           // entries loop follows the quadrant tests without a barrier (with the conversion over three waves below:
+           // pool k_render_bwd 642 -> 635 us, bitwise equal, profiles/r04/ab_bwd_conv)
             float4 *z = reinterpret_cast<float4 *>(myAcc);
             for (int q = lane; q < ZSLOT / 4; q += 64) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -967,13 +963,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)CH;
         }
         if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
-        if (WF && stager) s_ids[cur ^ 1][lane] = id_next;
         id_cur = id_next;
         id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
         static_assert(MB == 8, "one batch = two 4-entry list words");
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c1);
-        SEC_ADD(sec[1], ts_c0, ts_c1);  // chunk head: barriers, quadrant tests + compaction, next DMA issue
+        SEC_ADD(sec[2], ts_c0b, ts_c1);  // chunk head: quadrant tests + compaction, next DMA issue
 #endif
         const int lastrel = last - b0;  // this pixel's last contributor, relative to the chunk
         uint2 lraw[2];  // the next step's list words, read one step ahead
@@ -1050,97 +1045,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         }
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c2);
-        SEC_ADD(sec[2], ts_c1, ts_c2);  // the entries loop (evaluation, moments)
+        SEC_ADD(sec[3], ts_c1, ts_c2);  // the entries loop (evaluation, moments)
 #endif
-        if constexpr (WF) {
-        // Each wave turns ITS OWN moments (its quadrant's pixels only) into gradient partials and flushes them: the
-        // partials are linear in the moments, so the per-wave flushes add up, in the accumulators, to the tile's.
-        // No barrier between the entries loop and the atomics (the waves meet once per chunk, at its staging).
-        {
-            float *o = myWU;  // (dead after the entries loop until the next chunk's)
-            bool ndl = false;
-            if (lane < cnt) {
-                const int e = S.list[w][lane];
-                const float4 Pj = B.P[e];
-                const float4 Qj = B.Q[e];
-                float cA, cB, cC, op;
-                rec_conic(Pj, Qj, cA, cB, cC, op);
-                const float xg = Pj.x - cxT, yg = Pj.y - cyT;
-                const float *m = myAcc + e;
-                const float q0 = m[0], q1 = m[LS], q2 = m[2 * LS], q3 = m[3 * LS], q4 = m[4 * LS], q5 = m[5 * LS];
-                DetNorm nm;
-                if (DET) nm = det_norm(Pj.z, Pj.w, Qj.x, d.W, d.H);
-                const float Sx = fmaf(xg, q0, -q1), Sy = fmaf(yg, q0, -q2);
-                float p0 = -ddelx_dx * (cA * Sx + cB * Sy);
-                float p1 = -ddely_dy * (cC * Sy + cB * Sx);
-                float p5 = op > 0.f ? q0 / op : 0.f;
-                const float Sxx = fmaf(xg, fmaf(xg, q0, -2.f * q1), q3);
-                const float Sxy = fmaf(xg, fmaf(yg, q0, -q2), fmaf(-yg, q1, q4));
-                const float Syy = fmaf(yg, fmaf(yg, q0, -2.f * q2), q5);
-                float pc[3] = {-0.5f * Sxx, -0.5f * Sxy, -0.5f * Syy};
-                if (DET) {
-                    p0 = ldexpf(p0, det_s + nm.k[0]);
-                    p1 = ldexpf(p1, det_s + nm.k[1]);
-                    p5 = ldexpf(p5, det_s);
-#pragma unroll
-                    for (int qq = 0; qq < 3; qq++) pc[qq] = ldexpf(pc[qq], det_s + nm.k[2 + qq]);
-                }
-                o[0 * LS + lane] = p0;
-                o[1 * LS + lane] = p1;
-                o[5 * LS + lane] = p5;
-                ndl = !DET && rec_needle(Pj.z, Pj.w, Qj.x);
-#pragma unroll
-                for (int qq = 0; qq < 3; qq++) {
-                    o[(2 + qq) * LS + lane] = ndl ? 0.f : pc[qq];
-                    if (!DET) o[(NV + qq) * LS + lane] = ndl ? pc[qq] : 0.f;
-                }
-#pragma unroll
-                for (int qq = 6; qq < NV; qq++) {
-                    const float v = m[qq * LS] + m[(qq + NC) * LS];
-                    o[qq * LS + lane] = DET ? ldexpf(v, det_s) : v;
-                }
-            }
-            const bool any_ndl = __ballot(ndl) != 0ull;
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            int ft = lane;
-            asm volatile("" : "+v"(ft));  // (indices recomputed per chunk: hoisted, their offsets spilled)
-            for (int f = ft; f < cnt * NACC; f += 64) {
-                const int j = f / NACC, q = f - j * NACC;
-                if (q < NV) {
-                    const float a = o[q * LS + j];
-                    if (a != 0.f) {
-                        const unsigned gid = s_ids[cur][S.list[w][j]];
-                        const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
-                        if (DET) {
-                            if (!(fabsf(a) <= det_lim)) atomicAdd(det_sat, 1u);
-                            atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
-                                      (unsigned long long)__float2ll_rn(fminf(fmaxf(a, -9.0e18f), 9.0e18f)));
-                        } else {
-                            atomicAdd(accum + ai, a);
-                        }
-                    }
-                }
-            }
-            if (!DET && any_ndl) {  // (wave-uniform) this wave's needle conic partials, fp64
-                for (int f = ft; f < 3 * cnt; f += 64) {
-                    const int j = f % cnt, c3 = f / cnt;
-                    const float a = o[(NV + c3) * LS + j];
-                    if (a != 0.f) {
-                        const unsigned gid = s_ids[cur][S.list[w][j]];
-                        const size_t so = acc_side_offset(d.B, d.V, d.N) / 2;
-                        atomicAdd(reinterpret_cast<double *>(accum) + so + (gbase + gid) * 3 + c3, (double)a);
-                    }
-                }
-            }
-        }
-        // the next chunk's rows have landed before its barrier (the stagers' DMA)
-        vm_wait_all();
-#ifdef LGM_BWD_STAMPS
-        SEC_T(ts_c4);
-        SEC_ADD(sec[4], ts_c2, ts_c4);  // own partials + flush
-#endif
-        continue;
-        }
         __syncthreads();
         // moments -> gradient partials, an entry's three groups on three waves at once (thread 64 g + j, entry j):
         // g = 0 mean2D + opacity (moment rows 0..2), g = 1 conic (rows 0..5; a needle's go to rows NV..NV+2 for the
@@ -1207,11 +1113,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         }
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c3);
-        SEC_ADD(sec[3], ts_c2, ts_c3);  // barrier + moments -> partials
+        SEC_ADD(sec[4], ts_c2, ts_c3);  // barrier + moments -> partials
 #endif
         // the next chunk's DMA and ids have landed before the atomics below go out (they cannot delay it)
         vm_wait_all();
+#ifdef LGM_BWD_STAMPS
+        SEC_T(ts_c3a);
+        SEC_ADD(sec[5], ts_c3, ts_c3a);  // DMA wait (and any earlier outstanding vector-memory op of this wave)
+#endif
         __syncthreads();
+#ifdef LGM_BWD_STAMPS
+        SEC_T(ts_c3b);
+        SEC_ADD(sec[6], ts_c3a, ts_c3b);  // pre-flush barrier
+#endif
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
         constexpr int FT = 256;  // flushing threads
@@ -1260,13 +1174,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         }
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c4);
-        SEC_ADD(sec[4], ts_c3, ts_c4);  // DMA wait + barrier + gradient atomics
+        SEC_ADD(sec[7], ts_c3b, ts_c4);  // gradient atomics (issue)
 #endif
     }
 #ifdef LGM_BWD_STAMPS
     if (d.counters && lane == 0)
 #pragma unroll
-        for (int q = 0; q < 5; q++) atomicAdd(&d.counters[2 + q], sec[q]);
+        for (int q = 0; q < 8; q++) atomicAdd(&d.counters[q], sec[q]);
 #endif
     if (d.counters && tid == 0) {  // work-item timeline (lgm_diag.render_counters): start, end, (length | chunk | tile)
         unsigned long long *o = d.counters + item_stamps + 4 * (size_t)blockIdx.x;

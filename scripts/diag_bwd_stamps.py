@@ -29,9 +29,10 @@ for it in range(6):
         torch.autograd.backward([o["image"], o["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
         torch.cuda.synchronize()
     g.grad = None
-c = cnt[:10].tolist()
-names = ["prologue", "chunk_head", "entries", "partials", "flush"]
-tot = sum(c[2:7])
-res = {n: {"Gcyc": round(v / 1e9, 3), "share": round(v / max(tot, 1), 3)} for n, v in zip(names, c[2:7])}
+c = cnt[:8].tolist()
+names = ["prologue", "top_barrier", "chunk_head", "entries", "barrier_partials", "dma_wait", "flush_barrier",
+         "atomics"]
+tot = sum(c)
+res = {n: {"Gcyc": round(v / 1e9, 3), "share": round(v / max(tot, 1), 3)} for n, v in zip(names, c)}
 res["B"] = B
 print(json.dumps(res))

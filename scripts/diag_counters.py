@@ -31,9 +31,9 @@ with _native.diagnostics(render_counters=cnt):
     torch.autograd.backward([out["image"], out["alpha"]], [d_img.to(dev), d_alpha.to(dev)])
     torch.cuda.synchronize()
 c = cnt.tolist()
-# [0..7] hold only the LGM_BWD_STAMPS build's backward section cycles ([2..6], scripts/diag_bwd_stamps.py reads them);
+# [0..7] hold only the LGM_BWD_STAMPS build's backward section cycles (scripts/diag_bwd_stamps.py reads them);
 # the forward no longer writes aggregate counters there (include/lgm_render.h)
-res = {"bwd_section_cycles_stamps_build": c[2:7]} if any(c[:8]) else {}
+res = {"bwd_section_cycles_stamps_build": c[:8]} if any(c[:8]) else {}
 import numpy as np  # noqa: E402
 tl = np.array(c[8:8 + 8 * M], dtype=np.int64).reshape(M, 8)
 nl = tl[:, 6] & 0xFFFFFFFF

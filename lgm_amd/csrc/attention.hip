@@ -404,7 +404,8 @@ __global__ __launch_bounds__(NT) void k_attn_dkdv(int L, int H, float scale, con
 //     hardware transpose read), again shared by the QS sub-tiles;
 //   * row sums on the MFMA (ones^T P, on the same bf16/f16 P as the numerator), row max by max3 trees and the
 //     permlane16/32 swaps; masking only on the tail tile; the O rescale skipped while no row max grows;
-//   * K/V tiles double-buffered: the next tile's global loads are in flight during the current tile's MFMAs.
+//   * K/V tiles double-buffered: the next tile's global loads are in flight during the current tile's MFMAs (at
+//     D = 32 as LDS DMA straight into the other buffer, no staging registers: kv_swz).
 template <typename T, typename V4>
 __device__ __forceinline__ V4 tr_read(const T *p) {
     typedef __attribute__((ext_vector_type(4))) T TV4;
@@ -434,6 +435,64 @@ __device__ __forceinline__ typename Ty<DT>::V8 tr_frag(const typename Ty<DT>::T 
     typedef __attribute__((ext_vector_type(8))) short s8v;
     const s8v r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(V8, r);
+}
+
+// K/V tiles staged by LDS DMA (global_load_lds_dwordx4: lane i's 16 B land at M0 + 16 i, no VGPR staging) at
+// D = 32: unpadded 64-B rows whose four 16-B chunks are XOR-permuted by bit 2 of the row (logical chunk c of row r
+// sits at physical chunk c ^ kv_swz(r)). The permutation lives in each lane's SOURCE address (the DMA writes 1 KiB
+// contiguously); reads apply the same XOR. Row reads (ds_read_b128, lanes = rows 0..15 of one chunk) and the
+// transposed reads (ds_read_b64_tr_b16, 8 rows x 32 B per 32-lane half) are both conflict-free on it. Against register
+// staging into padded rows (the other head dims): bench level fwd / dQ / dK,dV -2.5 / -2.2 / -1.8 %, outputs bitwise
+// equal (profiles/r05/ab_attn_dma; held at 5 waves per SIMD the forward gained nothing more).
+__device__ __forceinline__ int kv_swz(int r) { return ((r >> 2) & 1) << 1; }
+__device__ __forceinline__ unsigned lds_addr32(const void *p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+// Issued from inline asm so that the compiler's waitcnt pass does not tie later LDS reads to the pending copy;
+// completion is ordered by vm_wait() + a barrier. M0 is saved and restored (the compiler owns it).
+__device__ __forceinline__ void lds_dma16(const void *src, unsigned lds_base) {
+    const unsigned m = __builtin_amdgcn_readfirstlane(lds_base);
+    unsigned saved;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(saved)
+                 : "s"(m), "v"(src)
+                 : "memory");
+}
+__device__ __forceinline__ void vm_wait() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+
+// tr_frag on the swizzled D = 32 image (row stride 32 elements); k0 a multiple of 32.
+template <int DT>
+__device__ __forceinline__ typename Ty<DT>::V8 tr_frag_swz(const typename Ty<DT>::T *tile, int k0, int d0, int lane) {
+    using T = typename Ty<DT>::T;
+    using V8 = typename Ty<DT>::V8;
+    const int g = lane >> 4, i = lane & 15;
+    const int row = k0 + 4 * g + (i >> 2), ch = (d0 >> 3) + ((i & 3) >> 1);
+    const T *p0 = tile + row * 32 + 8 * (ch ^ kv_swz(row)) + 4 * (i & 1);
+    typedef short s4v __attribute__((__vector_size__(8)));
+    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v *)(p0));
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v *)(p0 + 16 * 32));
+    typedef __attribute__((ext_vector_type(8))) short s8v;
+    const s8v r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(V8, r);
+}
+
+// One 64-row D = 32 tile of each of two [tokens][ld] tensors into their swizzled LDS images by DMA: wave w copies
+// rows 16 w .. 16 w + 15 (1 KiB per tensor); rows >= L read row L - 1 (finite; every consumer masks those rows:
+// scores -> -inf, P = 0). Asynchronous: valid after vm_wait() in every wave and a barrier.
+template <typename T>
+__device__ __forceinline__ void dma_tiles32(const T *pa, long long lda, const T *pb, long long ldb, int r0, int L,
+                                            T *ta, T *tb) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = 16 * w + (lane >> 2), c = (lane & 3) ^ kv_swz(r);
+    const long long row = min(r0 + r, L - 1);
+    lds_dma16(pa + row * lda + 8 * c, lds_addr32(ta) + 1024u * w);
+    lds_dma16(pb + row * ldb + 8 * c, lds_addr32(tb) + 1024u * w);
+}
+// The 16x16x32 row operand (row `row`, elements 8 g .. 8 g + 7) from a swizzled D = 32 image.
+template <int DT>
+__device__ __forceinline__ typename Ty<DT>::V8 row_frag_swz(const typename Ty<DT>::T *tile, int row, int g) {
+    return *reinterpret_cast<const typename Ty<DT>::V8 *>(tile + row * 32 + 8 * (g ^ kv_swz(row)));
 }
 
 // Waves per SIMD the compiler is held to (register cap 512 / n) for D <= 64; D = 128 stays at the compiler's
@@ -471,8 +530,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
                                                   typename Ty<DT>::T *__restrict__ o, float *__restrict__ lse) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr int LDK = D + LDK_PAD;                   // padded rows (see LDK_PAD)
-    constexpr int CH = 64 * D * 2 / 16 / NT;           // 16-B chunks per thread per tile (K or V)
+    constexpr bool DMA = D == 32;                      // LDS-DMA staging on the swizzled image (kv_swz)
+    constexpr int LDK = DMA ? D : D + LDK_PAD;         // padded rows (see LDK_PAD)
+    constexpr int CH = DMA ? 1 : 64 * D * 2 / 16 / NT;  // 16-B chunks per thread per tile (K or V)
     static_assert(CH >= 1, "tile too small for the loader");
     __shared__ __attribute__((aligned(16))) T Ks[2][64 * LDK];
     __shared__ __attribute__((aligned(16))) T Vs[2][64 * LDK];
@@ -480,6 +540,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
     const long long base = (long long)b * L * ld + (long long)h * D;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
     const int q0 = blockIdx.x * (64 * QS) + w * (16 * QS);
+    auto dma_tile = [&](int kb, int buf) { dma_tiles32(k + base, ld, v + base, ld, kb, L, Ks[buf], Vs[buf]); };
     const float c = scale * LOG2E;
     YFrag<DT, D> qf[QS];
 #pragma unroll
@@ -520,8 +581,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
             *reinterpret_cast<uint4 *>(&Vs[buf][r * LDK + col]) = vr[cc];
         }
     };
-    load_regs(0);
-    store_regs(0);
+    if constexpr (DMA) {
+        dma_tile(0, 0);
+        vm_wait();
+    } else {
+        load_regs(0);
+        store_regs(0);
+    }
     __syncthreads();
     int cur = 0;
     // one 64-key tile; TAIL: the last, partial tile (keys >= L masked): full tiles run a body without the masking
@@ -529,7 +595,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
     auto step = [&](int kb, auto tail) {
         constexpr bool TAIL = decltype(tail)::value;
         const bool more = kb + 64 < L;
-        if (more) load_regs(kb + 64);  // in flight during this tile's compute
+        if (more) {  // in flight during this tile's compute
+            if constexpr (DMA) dma_tile(kb + 64, cur ^ 1);  // (buffer cur^1 was last read before the previous barrier)
+            else load_regs(kb + 64);
+        }
         const T *Kt = Ks[cur], *Vt = Vs[cur];
         // ---- S^T sub-tiles (keys 16 sub + 4g + i, query r16 of sub-tile s)
         f32x4 sacc[QS][4];
@@ -538,7 +607,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
             V8 kf[D / 32];
 #pragma unroll
             for (int cc = 0; cc < D / 32; cc++)
-                kf[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                kf[cc] = DMA ? row_frag_swz<DT>(Kt, 16 * sub + r16, g)
+                             : *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
 #pragma unroll
             for (int s = 0; s < QS; s++) {
                 f32x4 a = {-m[s], -m[s], -m[s], -m[s]};  // the MFMA leaves exp2's argument itself
@@ -596,11 +666,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
         for (int t = 0; t < 2; t++)
 #pragma unroll
             for (int dt = 0; dt < D / 16; dt++) {
-                const V8 vf = tr_frag<DT>(Vt, LDK, 32 * t, 16 * dt, lane);
+                const V8 vf = DMA ? tr_frag_swz<DT>(Vt, 32 * t, 16 * dt, lane) : tr_frag<DT>(Vt, LDK, 32 * t, 16 * dt, lane);
 #pragma unroll
                 for (int s = 0; s < QS; s++) oacc[s][dt] = mfma32<DT>(vf, pb[s][t], oacc[s][dt]);
             }
-        if (more) store_regs(cur ^ 1);  // buffer cur^1 was last read before the previous barrier
+        if (more) {
+            if constexpr (DMA) vm_wait();  // this wave's copy landed (the barrier publishes every wave's)
+            else store_regs(cur ^ 1);     // buffer cur^1 was last read before the previous barrier
+        }
         __syncthreads();
         cur ^= 1;
     };
@@ -626,7 +699,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
 // ------------------------------------------------------------------------------------------------------------
 // backward, 16-bit inputs (v2). Both kernels read their tiles row-major from LDS only: the row reads feed the
 // S / dP products, the transposed operands (Q^T, dO^T, K^T) come from the same images via ds_read_b64_tr_b16.
-// Tiles are double-buffered through registers like the forward.
+// Tiles are double-buffered like the forward's (LDS DMA at D = 32, register staging otherwise).
 template <typename T, int D>
 struct TileLoader {  // one 64-row tile of up to two [tokens][ld] tensors, CH 16-B chunks per thread each
     static constexpr int CH = 64 * D * 2 / 16 / NT;
@@ -661,7 +734,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
                                                    typename Ty<DT>::T *__restrict__ dv, long long ldd) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr int LDK = D + LDK_PAD;
+    constexpr bool DMA = D == 32;  // LDS-DMA staging on the swizzled image (kv_swz)
+    constexpr int LDK = DMA ? D : D + LDK_PAD;
     __shared__ __attribute__((aligned(16))) T Qs[2][64 * LDK];  // Q * scale * log2(e), rounded (k_attn_dq2's qc)
     __shared__ __attribute__((aligned(16))) T Os[2][64 * LDK];
     __shared__ float sl[2][64], sd[2][64];
@@ -686,7 +760,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     TileLoader<T, D> ld_;
     float pl = 0.f, pd = 0.f;
     auto load_rows2 = [&](int qb) {
-        ld_.load(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L);
+        if constexpr (DMA)
+            dma_tiles32(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L, Qs[(qb >> 6) & 1],
+                        Os[(qb >> 6) & 1]);
+        else
+            ld_.load(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L);
         if (tid < 64) {
             const bool qv = qb + tid < L;
             pl = qv ? lse[(long long)bh * L + qb + tid] * LOG2E : INFINITY;  // invalid rows: P = 0
@@ -699,7 +777,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
         // fp64: 7.2e-3 vs 4.0e-3 rel L2, bf16 at L 4096; profiles/r05/attn_prescale). dK's product reads the same
         // image and is rescaled by scale / c at the end (a second, unscaled Q image cost +15 % dK,dV time; scaling
         // the staged tile here +8.5 %)
-        ld_.store(Qs[buf], Os[buf], LDK);
+        if constexpr (DMA) vm_wait();  // this wave's copies landed (the barrier publishes every wave's)
+        else ld_.store(Qs[buf], Os[buf], LDK);
         if (tid < 64) {  // stored negated: the accumulator inits
             // (the row index recomputed here: the two LDS addresses hoisted out of the query loop were spilled at the
             // 128-VGPR cap, and their scratch reloads sat on wave 0's path to every tile's barrier)
@@ -728,8 +807,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
                 V8 qr[D / 32], orr[D / 32];
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
-                    qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
-                    orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                    if constexpr (DMA) {
+                        qr[cc] = row_frag_swz<DT>(Qt, 16 * sub + r16, g);
+                        orr[cc] = row_frag_swz<DT>(Ot, 16 * sub + r16, g);
+                    } else {
+                        qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                        orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                    }
                 }
                 // (the accumulators start at -lse' / -delta of their rows q = 16 sub + 4 g + i, read as stored)
                 f32x4 ainit, dinit;
@@ -763,8 +847,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
                     }
 #pragma unroll
             for (int dt = 0; dt < D / 16; dt++) {
-                const V8 oT = tr_frag<DT>(Ot, LDK, 32 * t, 16 * dt, lane);  // dO^T
-                const V8 qT = tr_frag<DT>(Qt, LDK, 32 * t, 16 * dt, lane);  // Q^T
+                const V8 oT = DMA ? tr_frag_swz<DT>(Ot, 32 * t, 16 * dt, lane) : tr_frag<DT>(Ot, LDK, 32 * t, 16 * dt, lane);  // dO^T
+                const V8 qT = DMA ? tr_frag_swz<DT>(Qt, 32 * t, 16 * dt, lane) : tr_frag<DT>(Qt, LDK, 32 * t, 16 * dt, lane);  // Q^T
 #pragma unroll
                 for (int s = 0; s < KS; s++) {
                     dva[s][dt] = mfma32<DT>(oT, pb[s], dva[s][dt]);
@@ -805,7 +889,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                                                  typename Ty<DT>::T *__restrict__ qc) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr int LDK = D + LDK_PAD;
+    constexpr bool DMA = D == 32;  // LDS-DMA staging on the swizzled image (kv_swz)
+    constexpr int LDK = DMA ? D : D + LDK_PAD;
     __shared__ __attribute__((aligned(16))) T Ks[2][64 * LDK];
     __shared__ __attribute__((aligned(16))) T Vs[2][64 * LDK];
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -852,8 +937,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
 #pragma unroll
         for (int dt = 0; dt < D / 16; dt++) dqa[s][dt] = zero4();
     TileLoader<T, D> ld_;
-    ld_.load(k + base, ld, v + base, ld, 0, L);
-    ld_.store(Ks[0], Vs[0], LDK);
+    if constexpr (DMA) {
+        dma_tiles32(k + base, ld, v + base, ld, 0, L, Ks[0], Vs[0]);
+        vm_wait();
+    } else {
+        ld_.load(k + base, ld, v + base, ld, 0, L);
+        ld_.store(Ks[0], Vs[0], LDK);
+    }
     __syncthreads();
     int cur = 0;
     // one 64-key tile; TAIL: the last, partial tile (keys >= L masked) -- full tiles run a body without the masking
@@ -861,7 +951,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
     auto step = [&](int kb, auto tail_tag) {
         constexpr bool TAIL = decltype(tail_tag)::value;
         const bool more = kb + 64 < L;
-        if (more) ld_.load(k + base, ld, v + base, ld, kb + 64, L);
+        if (more) {
+            if constexpr (DMA) dma_tiles32(k + base, ld, v + base, ld, kb + 64, L, Ks[cur ^ 1], Vs[cur ^ 1]);
+            else ld_.load(k + base, ld, v + base, ld, kb + 64, L);
+        }
         const T *Kt = Ks[cur], *Vt = Vs[cur];
         // the tile's two 32-key halves one after the other (half the score registers live at once)
 #pragma unroll
@@ -873,8 +966,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                 V8 kr[D / 32], vr[D / 32];
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
-                    kr[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
-                    vr[cc] = *reinterpret_cast<const V8 *>(Vt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                    if constexpr (DMA) {
+                        kr[cc] = row_frag_swz<DT>(Kt, 16 * sub + r16, g);
+                        vr[cc] = row_frag_swz<DT>(Vt, 16 * sub + r16, g);
+                    } else {
+                        kr[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                        vr[cc] = *reinterpret_cast<const V8 *>(Vt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
+                    }
                 }
 #pragma unroll
                 for (int s = 0; s < QS; s++) {
@@ -904,12 +1002,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                 }
 #pragma unroll
             for (int dt = 0; dt < D / 16; dt++) {
-                const V8 kT = tr_frag<DT>(Kt, LDK, 32 * t, 16 * dt, lane);  // K^T
+                const V8 kT = DMA ? tr_frag_swz<DT>(Kt, 32 * t, 16 * dt, lane) : tr_frag<DT>(Kt, LDK, 32 * t, 16 * dt, lane);  // K^T
 #pragma unroll
                 for (int s = 0; s < QS; s++) dqa[s][dt] = mfma32<DT>(kT, db[s], dqa[s][dt]);
             }
         }
-        if (more) ld_.store(Ks[cur ^ 1], Vs[cur ^ 1], LDK);
+        if (more) {
+            if constexpr (DMA) vm_wait();  // this wave's copies landed (the barrier publishes every wave's)
+            else ld_.store(Ks[cur ^ 1], Vs[cur ^ 1], LDK);
+        }
         __syncthreads();
         cur ^= 1;
     };

@@ -438,13 +438,19 @@ __device__ __forceinline__ typename Ty<DT>::V8 tr_frag(const typename Ty<DT>::T 
 }
 
 // K/V tiles staged by LDS DMA (global_load_lds_dwordx4: lane i's 16 B land at M0 + 16 i, no VGPR staging) at
-// D = 32: unpadded 64-B rows whose four 16-B chunks are XOR-permuted by bit 2 of the row (logical chunk c of row r
-// sits at physical chunk c ^ kv_swz(r)). The permutation lives in each lane's SOURCE address (the DMA writes 1 KiB
-// contiguously); reads apply the same XOR. Row reads (ds_read_b128, lanes = rows 0..15 of one chunk) and the
-// transposed reads (ds_read_b64_tr_b16, 8 rows x 32 B per 32-lane half) are both conflict-free on it. Against register
-// staging into padded rows (the other head dims): bench level fwd / dQ / dK,dV -2.5 / -2.2 / -1.8 %, outputs bitwise
-// equal (profiles/r05/ab_attn_dma; held at 5 waves per SIMD the forward gained nothing more).
-__device__ __forceinline__ int kv_swz(int r) { return ((r >> 2) & 1) << 1; }
+// D = 32 and 64: unpadded rows (64 / 128 B) whose 16-B chunks are XOR-permuted by row bits (logical chunk c of row r
+// sits at physical chunk c ^ kv_swz<D>(r)). The permutation lives in each lane's SOURCE address (the DMA writes
+// 1 KiB contiguously); reads apply the same XOR. Row reads (ds_read_b128, lanes = rows 0..15 of one chunk) and the
+// transposed reads (ds_read_b64_tr_b16, 8 rows x 32 B per 32-lane half) are both conflict-free on it by the bank
+// rule of MI355X_MICROARCH §LDS (checked exhaustively for both widths). Against register staging into padded rows
+// (D = 128 keeps that): bench level fwd / dQ / dK,dV -2.5 / -2.2 / -1.8 % at D = 32, outputs bitwise equal
+// (profiles/r05/ab_attn_dma; held at 5 waves per SIMD the forward gained nothing more); at D = 64 (LGM's C = 1024
+// levels) fwd / dQ / dK,dV -2…-10 / -5…-7 / -3…-6 % (profiles/r05/ab_attn_d64).
+template <int D>
+__device__ __forceinline__ int kv_swz(int r) {
+    if constexpr (D == 32) return ((r >> 2) & 1) << 1;       // rows r, r + 4 of a transposed read: other 32 B
+    else return (((r >> 1) & 3) << 1) | ((r >> 2) & 1);       // D = 64: two rows per 256-B bank line
+}
 __device__ __forceinline__ unsigned lds_addr32(const void *p) {
     return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }
@@ -461,38 +467,42 @@ __device__ __forceinline__ void lds_dma16(const void *src, unsigned lds_base) {
 }
 __device__ __forceinline__ void vm_wait() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
-// tr_frag on the swizzled D = 32 image (row stride 32 elements); k0 a multiple of 32.
-template <int DT>
+// One 64-row tile of each of two [tokens][ld] tensors into their swizzled LDS images by DMA: wave w copies rows
+// 16 w .. 16 w + 15 (D / 32 pieces of 1 KiB per tensor); rows >= L read row L - 1 (finite; every consumer masks
+// those rows: scores -> -inf, P = 0). Asynchronous: valid after vm_wait() in every wave and a barrier.
+template <int D, typename T>
+__device__ __forceinline__ void dma_tiles(const T *pa, long long lda, const T *pb, long long ldb, int r0, int L, T *ta,
+                                          T *tb) {
+    constexpr int CPR = D / 8;  // 16-B chunks per row
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < D / 32; j++) {
+        const int slot = w * 16 * CPR + j * 64 + lane;  // 16-B slot of the image this lane fills
+        const int r = slot / CPR, c = (slot % CPR) ^ kv_swz<D>(r);
+        const long long row = min(r0 + r, L - 1);
+        lds_dma16(pa + row * lda + 8 * c, lds_addr32(ta) + 1024u * (w * (D / 32) + j));
+        lds_dma16(pb + row * ldb + 8 * c, lds_addr32(tb) + 1024u * (w * (D / 32) + j));
+    }
+}
+// The 16x16x32 row operand (row `row`, logical 16-B chunk `ch`) from a swizzled image.
+template <int DT, int D>
+__device__ __forceinline__ typename Ty<DT>::V8 row_frag_swz(const typename Ty<DT>::T *tile, int row, int ch) {
+    return *reinterpret_cast<const typename Ty<DT>::V8 *>(tile + row * D + 8 * (ch ^ kv_swz<D>(row)));
+}
+// tr_frag on a swizzled image; k0 a multiple of 32.
+template <int DT, int D>
 __device__ __forceinline__ typename Ty<DT>::V8 tr_frag_swz(const typename Ty<DT>::T *tile, int k0, int d0, int lane) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
     const int g = lane >> 4, i = lane & 15;
     const int row = k0 + 4 * g + (i >> 2), ch = (d0 >> 3) + ((i & 3) >> 1);
-    const T *p0 = tile + row * 32 + 8 * (ch ^ kv_swz(row)) + 4 * (i & 1);
+    const T *p0 = tile + row * D + 8 * (ch ^ kv_swz<D>(row)) + 4 * (i & 1);
     typedef short s4v __attribute__((__vector_size__(8)));
     const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v *)(p0));
-    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v *)(p0 + 16 * 32));
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v *)(p0 + 16 * D));
     typedef __attribute__((ext_vector_type(8))) short s8v;
     const s8v r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(V8, r);
-}
-
-// One 64-row D = 32 tile of each of two [tokens][ld] tensors into their swizzled LDS images by DMA: wave w copies
-// rows 16 w .. 16 w + 15 (1 KiB per tensor); rows >= L read row L - 1 (finite; every consumer masks those rows:
-// scores -> -inf, P = 0). Asynchronous: valid after vm_wait() in every wave and a barrier.
-template <typename T>
-__device__ __forceinline__ void dma_tiles32(const T *pa, long long lda, const T *pb, long long ldb, int r0, int L,
-                                            T *ta, T *tb) {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = 16 * w + (lane >> 2), c = (lane & 3) ^ kv_swz(r);
-    const long long row = min(r0 + r, L - 1);
-    lds_dma16(pa + row * lda + 8 * c, lds_addr32(ta) + 1024u * w);
-    lds_dma16(pb + row * ldb + 8 * c, lds_addr32(tb) + 1024u * w);
-}
-// The 16x16x32 row operand (row `row`, elements 8 g .. 8 g + 7) from a swizzled D = 32 image.
-template <int DT>
-__device__ __forceinline__ typename Ty<DT>::V8 row_frag_swz(const typename Ty<DT>::T *tile, int row, int g) {
-    return *reinterpret_cast<const typename Ty<DT>::V8 *>(tile + row * 32 + 8 * (g ^ kv_swz(row)));
 }
 
 // Waves per SIMD the compiler is held to (register cap 512 / n) for D <= 64; D = 128 stays at the compiler's
@@ -530,7 +540,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
                                                   typename Ty<DT>::T *__restrict__ o, float *__restrict__ lse) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr bool DMA = D == 32;                      // LDS-DMA staging on the swizzled image (kv_swz)
+    constexpr bool DMA = D == 32 || D == 64;                      // LDS-DMA staging on the swizzled image (kv_swz)
     constexpr int LDK = DMA ? D : D + LDK_PAD;         // padded rows (see LDK_PAD)
     constexpr int CH = DMA ? 1 : 64 * D * 2 / 16 / NT;  // 16-B chunks per thread per tile (K or V)
     static_assert(CH >= 1, "tile too small for the loader");
@@ -540,7 +550,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
     const long long base = (long long)b * L * ld + (long long)h * D;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
     const int q0 = blockIdx.x * (64 * QS) + w * (16 * QS);
-    auto dma_tile = [&](int kb, int buf) { dma_tiles32(k + base, ld, v + base, ld, kb, L, Ks[buf], Vs[buf]); };
+    auto dma_tile = [&](int kb, int buf) { dma_tiles<D>(k + base, ld, v + base, ld, kb, L, Ks[buf], Vs[buf]); };
     const float c = scale * LOG2E;
     YFrag<DT, D> qf[QS];
 #pragma unroll
@@ -607,7 +617,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
             V8 kf[D / 32];
 #pragma unroll
             for (int cc = 0; cc < D / 32; cc++)
-                kf[cc] = DMA ? row_frag_swz<DT>(Kt, 16 * sub + r16, g)
+                kf[cc] = DMA ? row_frag_swz<DT, D>(Kt, 16 * sub + r16, 4 * cc + g)
                              : *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
 #pragma unroll
             for (int s = 0; s < QS; s++) {
@@ -666,7 +676,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
         for (int t = 0; t < 2; t++)
 #pragma unroll
             for (int dt = 0; dt < D / 16; dt++) {
-                const V8 vf = DMA ? tr_frag_swz<DT>(Vt, 32 * t, 16 * dt, lane) : tr_frag<DT>(Vt, LDK, 32 * t, 16 * dt, lane);
+                const V8 vf = DMA ? tr_frag_swz<DT, D>(Vt, 32 * t, 16 * dt, lane) : tr_frag<DT>(Vt, LDK, 32 * t, 16 * dt, lane);
 #pragma unroll
                 for (int s = 0; s < QS; s++) oacc[s][dt] = mfma32<DT>(vf, pb[s][t], oacc[s][dt]);
             }
@@ -734,7 +744,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
                                                    typename Ty<DT>::T *__restrict__ dv, long long ldd) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr bool DMA = D == 32;  // LDS-DMA staging on the swizzled image (kv_swz)
+    constexpr bool DMA = D == 32 || D == 64;  // LDS-DMA staging on the swizzled image (kv_swz)
     constexpr int LDK = DMA ? D : D + LDK_PAD;
     __shared__ __attribute__((aligned(16))) T Qs[2][64 * LDK];  // Q * scale * log2(e), rounded (k_attn_dq2's qc)
     __shared__ __attribute__((aligned(16))) T Os[2][64 * LDK];
@@ -761,7 +771,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
     float pl = 0.f, pd = 0.f;
     auto load_rows2 = [&](int qb) {
         if constexpr (DMA)
-            dma_tiles32(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L, Qs[(qb >> 6) & 1],
+            dma_tiles<D>(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L, Qs[(qb >> 6) & 1],
                         Os[(qb >> 6) & 1]);
         else
             ld_.load(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L);
@@ -808,8 +818,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
                     if constexpr (DMA) {
-                        qr[cc] = row_frag_swz<DT>(Qt, 16 * sub + r16, g);
-                        orr[cc] = row_frag_swz<DT>(Ot, 16 * sub + r16, g);
+                        qr[cc] = row_frag_swz<DT, D>(Qt, 16 * sub + r16, 4 * cc + g);
+                        orr[cc] = row_frag_swz<DT, D>(Ot, 16 * sub + r16, 4 * cc + g);
                     } else {
                         qr[cc] = *reinterpret_cast<const V8 *>(Qt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
                         orr[cc] = *reinterpret_cast<const V8 *>(Ot + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
@@ -847,8 +857,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
                     }
 #pragma unroll
             for (int dt = 0; dt < D / 16; dt++) {
-                const V8 oT = DMA ? tr_frag_swz<DT>(Ot, 32 * t, 16 * dt, lane) : tr_frag<DT>(Ot, LDK, 32 * t, 16 * dt, lane);  // dO^T
-                const V8 qT = DMA ? tr_frag_swz<DT>(Qt, 32 * t, 16 * dt, lane) : tr_frag<DT>(Qt, LDK, 32 * t, 16 * dt, lane);  // Q^T
+                const V8 oT = DMA ? tr_frag_swz<DT, D>(Ot, 32 * t, 16 * dt, lane) : tr_frag<DT>(Ot, LDK, 32 * t, 16 * dt, lane);  // dO^T
+                const V8 qT = DMA ? tr_frag_swz<DT, D>(Qt, 32 * t, 16 * dt, lane) : tr_frag<DT>(Qt, LDK, 32 * t, 16 * dt, lane);  // Q^T
 #pragma unroll
                 for (int s = 0; s < KS; s++) {
                     dva[s][dt] = mfma32<DT>(oT, pb[s], dva[s][dt]);
@@ -889,7 +899,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                                                  typename Ty<DT>::T *__restrict__ qc) {
     using T = typename Ty<DT>::T;
     using V8 = typename Ty<DT>::V8;
-    constexpr bool DMA = D == 32;  // LDS-DMA staging on the swizzled image (kv_swz)
+    constexpr bool DMA = D == 32 || D == 64;  // LDS-DMA staging on the swizzled image (kv_swz)
     constexpr int LDK = DMA ? D : D + LDK_PAD;
     __shared__ __attribute__((aligned(16))) T Ks[2][64 * LDK];
     __shared__ __attribute__((aligned(16))) T Vs[2][64 * LDK];
@@ -938,7 +948,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         for (int dt = 0; dt < D / 16; dt++) dqa[s][dt] = zero4();
     TileLoader<T, D> ld_;
     if constexpr (DMA) {
-        dma_tiles32(k + base, ld, v + base, ld, 0, L, Ks[0], Vs[0]);
+        dma_tiles<D>(k + base, ld, v + base, ld, 0, L, Ks[0], Vs[0]);
         vm_wait();
     } else {
         ld_.load(k + base, ld, v + base, ld, 0, L);
@@ -952,7 +962,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         constexpr bool TAIL = decltype(tail_tag)::value;
         const bool more = kb + 64 < L;
         if (more) {
-            if constexpr (DMA) dma_tiles32(k + base, ld, v + base, ld, kb + 64, L, Ks[cur ^ 1], Vs[cur ^ 1]);
+            if constexpr (DMA) dma_tiles<D>(k + base, ld, v + base, ld, kb + 64, L, Ks[cur ^ 1], Vs[cur ^ 1]);
             else ld_.load(k + base, ld, v + base, ld, kb + 64, L);
         }
         const T *Kt = Ks[cur], *Vt = Vs[cur];
@@ -967,8 +977,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
 #pragma unroll
                 for (int cc = 0; cc < D / 32; cc++) {
                     if constexpr (DMA) {
-                        kr[cc] = row_frag_swz<DT>(Kt, 16 * sub + r16, g);
-                        vr[cc] = row_frag_swz<DT>(Vt, 16 * sub + r16, g);
+                        kr[cc] = row_frag_swz<DT, D>(Kt, 16 * sub + r16, 4 * cc + g);
+                        vr[cc] = row_frag_swz<DT, D>(Vt, 16 * sub + r16, 4 * cc + g);
                     } else {
                         kr[cc] = *reinterpret_cast<const V8 *>(Kt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
                         vr[cc] = *reinterpret_cast<const V8 *>(Vt + (16 * sub + r16) * LDK + 32 * cc + 8 * g);
@@ -1002,7 +1012,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                 }
 #pragma unroll
             for (int dt = 0; dt < D / 16; dt++) {
-                const V8 kT = DMA ? tr_frag_swz<DT>(Kt, 32 * t, 16 * dt, lane) : tr_frag<DT>(Kt, LDK, 32 * t, 16 * dt, lane);  // K^T
+                const V8 kT = DMA ? tr_frag_swz<DT, D>(Kt, 32 * t, 16 * dt, lane) : tr_frag<DT>(Kt, LDK, 32 * t, 16 * dt, lane);  // K^T
 #pragma unroll
                 for (int s = 0; s < QS; s++) dqa[s][dt] = mfma32<DT>(kT, db[s], dqa[s][dt]);
             }
@@ -1035,9 +1045,19 @@ int fwd_impl(int B, int L, int H, float scale, const void *q, const void *k, con
              float *lse, hipStream_t st) {
     using T = typename Ty<DT>::T;
     if constexpr (DT != LGM_ATTN_F32) {
-        // two query sub-tiles per wavefront when the grid stays large enough to fill the chip
+        // two query sub-tiles per wavefront when the grid stays large enough to fill the chip; at D = 32 four (64
+        // queries per wave, 3 waves per SIMD at 168 VGPRs: each K fragment and V^T fragment read from LDS feeds four
+        // MFMAs) once the grid covers two rounds of the 768 workgroup slots: bench level (2,048 workgroups)
+        // k_attn_fwd -5 % against two, but cfg4's L = 9,600 (608 workgroups, a fifth of the slots idle) +10 %
+        // (profiles/r05/ab_attn_qs; three sub-tiles measured slower, and the same widening of dQ / dK,dV gained nothing)
+        constexpr int QS4 = D == 32 ? 4 : 0;
         constexpr int QS2 = D <= 64 ? 2 : 1;
-        if (QS2 == 2 && (long long)((L + 127) / 128) * B * H >= QS_MIN_GRID) {
+        constexpr long long QS4_MIN_GRID = 1536;
+        if (QS4 && (long long)((L + 255) / 256) * B * H >= QS4_MIN_GRID) {
+            dim3 grid((L + 255) / 256, B * H);
+            LGM_LAUNCH("k_attn_fwd", st, (k_attn_fwd2<DT, D, (QS4 ? QS4 : 1)><<<grid, NT, 0, st>>>(
+                                              L, H, scale, (const T *)q, (const T *)k, (const T *)v, ld, (T *)o, lse)));
+        } else if (QS2 == 2 && (long long)((L + 127) / 128) * B * H >= QS_MIN_GRID) {
             dim3 grid((L + 127) / 128, B * H);
             LGM_LAUNCH("k_attn_fwd", st, (k_attn_fwd2<DT, D, QS2><<<grid, NT, 0, st>>>(
                                               L, H, scale, (const T *)q, (const T *)k, (const T *)v, ld, (T *)o, lse)));

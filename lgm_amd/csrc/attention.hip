@@ -484,6 +484,35 @@ __device__ __forceinline__ void dma_tiles(const T *pa, long long lda, const T *p
         lds_dma16(pb + row * ldb + 8 * c, lds_addr32(tb) + 1024u * (w * (D / 32) + j));
     }
 }
+// dma_tiles for a tile loop: this lane's source offsets inside tile 0 are computed once; a full tile adds the
+// (uniform) tile offset to them, only a tile reaching past L recomputes with the row clamp.
+template <int D, typename T>
+struct DmaStream {
+    const T *pa, *pb;
+    long long lda, ldb;
+    int oa, ob;  // this lane's element offsets in tile 0 (its row and swizzled chunk)
+    __device__ __forceinline__ DmaStream(const T *a, long long la, const T *b, long long lb)
+        : pa(a), pb(b), lda(la), ldb(lb) {
+        constexpr int CPR = D / 8;
+        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int slot = w * 16 * CPR + lane, r = slot / CPR, c = (slot % CPR) ^ kv_swz<D>(r);
+        oa = (int)(r * la) + 8 * c;
+        ob = (int)(r * lb) + 8 * c;
+    }
+    __device__ __forceinline__ void issue(int r0, int L, T *ta, T *tb) const {
+        if (r0 + 64 <= L) {  // workgroup-uniform
+            const int w = threadIdx.x >> 6;
+            constexpr int RPP = 512 / D;  // rows per 1-KiB piece
+#pragma unroll
+            for (int j = 0; j < D / 32; j++) {
+                lds_dma16(pa + (r0 + j * RPP) * lda + oa, lds_addr32(ta) + 1024u * (w * (D / 32) + j));
+                lds_dma16(pb + (r0 + j * RPP) * ldb + ob, lds_addr32(tb) + 1024u * (w * (D / 32) + j));
+            }
+        } else {
+            dma_tiles<D>(pa, lda, pb, ldb, r0, L, ta, tb);
+        }
+    }
+};
 // The 16x16x32 row operand (row `row`, logical 16-B chunk `ch`) from a swizzled image.
 template <int DT, int D>
 __device__ __forceinline__ typename Ty<DT>::V8 row_frag_swz(const typename Ty<DT>::T *tile, int row, int ch) {
@@ -533,6 +562,27 @@ __device__ __forceinline__ void prescale(typename Ty<DT>::V8 (&v)[N], float c) {
         for (int j = 0; j < 8; j++) v[a][j] = (typename Ty<DT>::T)((float)v[a][j] * c);
 }
 constexpr long long QS_MIN_GRID = 512;  // two query sub-tiles per wave once the grid has this many workgroups
+// The key-tile loop of the forward and dQ kernels: step(kb, tail, buffer) over the 64-key tiles, full tiles first,
+// the buffer index alternating from 0 as a compile-time constant (the two buffers' bodies run in turn).
+template <class Step>
+__device__ __forceinline__ void tile_loop(int L, Step &&step) {
+    using F = std::false_type;
+    using Tr = std::true_type;
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    const int kfull = L & ~63;
+    int kb = 0;
+    for (; kb + 128 <= kfull; kb += 128) {
+        step(kb, F{}, B0{});
+        step(kb + 64, F{}, B1{});
+    }
+    if (kb < kfull) {  // one more full tile (buffer 0), then the tail in buffer 1
+        step(kb, F{}, B0{});
+        if (kfull < L) step(kfull, Tr{}, B1{});
+    } else if (kfull < L) {
+        step(kfull, Tr{}, B0{});
+    }
+}
 template <int DT, int D, int QS>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FWD_WPE : 1))) void k_attn_fwd2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
                                                   const typename Ty<DT>::T *__restrict__ k,
@@ -550,7 +600,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
     const long long base = (long long)b * L * ld + (long long)h * D;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
     const int q0 = blockIdx.x * (64 * QS) + w * (16 * QS);
-    auto dma_tile = [&](int kb, int buf) { dma_tiles<D>(k + base, ld, v + base, ld, kb, L, Ks[buf], Vs[buf]); };
+    const DmaStream<D, T> dsrc(k + base, ld, v + base, ld);
+    auto dma_tile = [&](int kb, int buf) { dsrc.issue(kb, L, Ks[buf], Vs[buf]); };
     const float c = scale * LOG2E;
     YFrag<DT, D> qf[QS];
 #pragma unroll
@@ -599,11 +650,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
         store_regs(0);
     }
     __syncthreads();
-    int cur = 0;
-    // one 64-key tile; TAIL: the last, partial tile (keys >= L masked): full tiles run a body without the masking
-    // code. (An unconditional rescale instead of the branch below measured the same: profiles/r02/ab_attn_pad.)
-    auto step = [&](int kb, auto tail) {
+    // one 64-key tile read from buffer CUR; TAIL: the last, partial tile (keys >= L masked): full tiles run a body
+    // without the masking code. (An unconditional rescale instead of the branch below measured the same:
+    // profiles/r02/ab_attn_pad.) CUR is a compile-time index (tile_loop runs the two buffers' bodies in turn), so
+    // every LDS address is a per-lane base plus an immediate.
+    auto step = [&](int kb, auto tail, auto cur_tag) {
         constexpr bool TAIL = decltype(tail)::value;
+        constexpr int cur = decltype(cur_tag)::value;
         const bool more = kb + 64 < L;
         if (more) {  // in flight during this tile's compute
             if constexpr (DMA) dma_tile(kb + 64, cur ^ 1);  // (buffer cur^1 was last read before the previous barrier)
@@ -685,11 +738,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FW
             else store_regs(cur ^ 1);     // buffer cur^1 was last read before the previous barrier
         }
         __syncthreads();
-        cur ^= 1;
     };
-    const int kfull = L & ~63;
-    for (int kb = 0; kb < kfull; kb += 64) step(kb, std::false_type{});
-    if (kfull < L) step(kfull, std::true_type{});
+    tile_loop(L, step);
 #pragma unroll
     for (int s = 0; s < QS; s++) {
         const int qr = q0 + 16 * s + r16;
@@ -769,10 +819,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
         for (int dt = 0; dt < D / 16; dt++) { dka[s][dt] = zero4(); dva[s][dt] = zero4(); }
     TileLoader<T, D> ld_;
     float pl = 0.f, pd = 0.f;
-    auto load_rows2 = [&](int qb) {
+    const DmaStream<D, T> dsrc(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D);
+    auto load_rows2 = [&](int qb, int buf) {
         if constexpr (DMA)
-            dma_tiles<D>(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L, Qs[(qb >> 6) & 1],
-                        Os[(qb >> 6) & 1]);
+            dsrc.issue(qb, L, Qs[buf], Os[buf]);
         else
             ld_.load(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L);
         if (tid < 64) {
@@ -798,13 +848,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
             sd[buf][row] = -pd;
         }
     };
-    load_rows2(0);
+    load_rows2(0, 0);
     store_rows2(0);
     __syncthreads();
-    int cur = 0;
-    for (int qb = 0; qb < L; qb += 64) {
+    // one 64-query tile read from buffer CUR (a compile-time index: the loop below runs the two buffers' bodies in
+    // turn, so every LDS address is a per-lane base plus an immediate)
+    auto tile = [&](int qb, auto cur_tag) {
+        constexpr int cur = decltype(cur_tag)::value;
         const bool more = qb + 64 < L;
-        if (more) load_rows2(qb + 64);
+        if (more) load_rows2(qb + 64, cur ^ 1);
         const T *Qt = Qs[cur], *Ot = Os[cur];  // (dK from Q * c: rescaled below)
         // the tile's two 32-query halves one after the other (S / dP of subs 2t, 2t + 1, then their dV / dK
         // products): half the score registers live at once (dK,dV at D = 32 fits 4 waves per SIMD instead of 3)
@@ -868,7 +920,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
         }
         if (more) store_rows2(cur ^ 1);
         __syncthreads();
-        cur ^= 1;
+    };
+    for (int qb = 0; qb < L; qb += 128) {
+        tile(qb, std::integral_constant<int, 0>{});
+        if (qb + 64 < L) tile(qb + 64, std::integral_constant<int, 1>{});
     }
 #pragma unroll
     for (int s = 0; s < KS; s++) {
@@ -955,14 +1010,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         ld_.store(Ks[0], Vs[0], LDK);
     }
     __syncthreads();
-    int cur = 0;
-    // one 64-key tile; TAIL: the last, partial tile (keys >= L masked) -- full tiles run a body without the masking
-    // (a runtime tail flag left ~70 compare / select VALU per tile in the main loop)
-    auto step = [&](int kb, auto tail_tag) {
+    const DmaStream<D, T> dsrc(k + base, ld, v + base, ld);
+    // one 64-key tile read from buffer CUR (compile-time: tile_loop); TAIL: the last, partial tile (keys >= L masked)
+    // -- full tiles run a body without the masking (a runtime tail flag left ~70 compare / select VALU per tile in
+    // the main loop)
+    auto step = [&](int kb, auto tail_tag, auto cur_tag) {
         constexpr bool TAIL = decltype(tail_tag)::value;
+        constexpr int cur = decltype(cur_tag)::value;
         const bool more = kb + 64 < L;
         if (more) {
-            if constexpr (DMA) dma_tiles<D>(k + base, ld, v + base, ld, kb + 64, L, Ks[cur ^ 1], Vs[cur ^ 1]);
+            if constexpr (DMA) dsrc.issue(kb + 64, L, Ks[cur ^ 1], Vs[cur ^ 1]);
             else ld_.load(k + base, ld, v + base, ld, kb + 64, L);
         }
         const T *Kt = Ks[cur], *Vt = Vs[cur];
@@ -1022,11 +1079,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
             else ld_.store(Ks[cur ^ 1], Vs[cur ^ 1], LDK);
         }
         __syncthreads();
-        cur ^= 1;
     };
-    const int kfull = L & ~63;
-    for (int kb = 0; kb < kfull; kb += 64) step(kb, std::false_type{});
-    if (kfull < L) step(kfull, std::true_type{});
+    tile_loop(L, step);
 #pragma unroll
     for (int s = 0; s < QS; s++) {
         const int qr = q0 + 16 * s + r16;

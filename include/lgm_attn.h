@@ -31,9 +31,9 @@ extern "C" {
 #define LGM_ATTN_BF16 1
 #define LGM_ATTN_F16 2
 
-/* Bytes of device scratch lgm_attn_backward needs: the fp32 delta = rowsum(dO * O) buffer, and for 16-bit dtypes
- * the rounded Q * scale * log2(e) rows the dQ pass hands to the dK/dV pass (both recompute the forward's P from the
- * same rounded operands). */
+/* Bytes of device scratch lgm_attn_backward needs: fp32: the delta = rowsum(dO * O) buffer; 16-bit dtypes: the
+ * per-row constants the dQ pass hands to the dK/dV pass (-lse * log2(e) and -delta, rows padded to a multiple of 64)
+ * and the rounded Q * scale * log2(e) rows (both passes recompute the forward's P from the same rounded operands). */
 size_t lgm_attn_workspace_size(int dtype, int B, int L, int H, int D);
 
 /* o = softmax(scale * q k^T) v per (batch, head); also writes lse. */

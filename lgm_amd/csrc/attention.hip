@@ -466,6 +466,20 @@ __device__ __forceinline__ void lds_dma16(const void *src, unsigned lds_base) {
                  : "memory");
 }
 __device__ __forceinline__ void vm_wait() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+// The 4-byte form: lane i's dword lands at M0 + 4 i (64 consecutive floats per wave-instruction).
+__device__ __forceinline__ void lds_dma4(const void *src, unsigned lds_base) {
+    const unsigned m = __builtin_amdgcn_readfirstlane(lds_base);
+    unsigned saved;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %2, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(saved)
+                 : "s"(m), "v"(src)
+                 : "memory");
+}
+// Per-row constants the dK,dV pass needs, written by k_attn_dq2 (16-bit paths): -lse * log2(e) and -delta of every
+// query row, [B*H][Lp] each (Lp = L rounded up to 64; rows >= L hold -inf and 0, so P = 0 there), DMA'd with each
+// query tile instead of loaded, negated and stored by one wave.
+__host__ __device__ __forceinline__ int row_pitch(int L) { return (L + 63) & ~63; }
 
 // One 64-row tile of each of two [tokens][ld] tensors into their swizzled LDS images by DMA: wave w copies rows
 // 16 w .. 16 w + 15 (D / 32 pieces of 1 KiB per tensor); rows >= L read row L - 1 (finite; every consumer masks
@@ -789,7 +803,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
                                                    const typename Ty<DT>::T *__restrict__ k,
                                                    const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                    const typename Ty<DT>::T *__restrict__ dout,
-                                                   const float *__restrict__ lse, const float *__restrict__ delta,
+                                                   const float *__restrict__ nrow,
                                                    typename Ty<DT>::T *__restrict__ dk,
                                                    typename Ty<DT>::T *__restrict__ dv, long long ldd) {
     using T = typename Ty<DT>::T;
@@ -818,17 +832,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
 #pragma unroll
         for (int dt = 0; dt < D / 16; dt++) { dka[s][dt] = zero4(); dva[s][dt] = zero4(); }
     TileLoader<T, D> ld_;
-    float pl = 0.f, pd = 0.f;
     const DmaStream<D, T> dsrc(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D);
+    const int Lp = row_pitch(L);
+    const float *nl2 = nrow + (long long)bh * Lp + lane, *nd = nl2 + (long long)gridDim.y * Lp;
     auto load_rows2 = [&](int qb, int buf) {
         if constexpr (DMA)
             dsrc.issue(qb, L, Qs[buf], Os[buf]);
         else
             ld_.load(qc + (long long)bh * L * D, D, dout + obase, (long long)H * D, qb, L);
-        if (tid < 64) {
-            const bool qv = qb + tid < L;
-            pl = qv ? lse[(long long)bh * L + qb + tid] * LOG2E : INFINITY;  // invalid rows: P = 0
-            pd = qv ? delta[(long long)bh * L + qb + tid] : 0.f;
+        if (w == 0) {  // the tile's -lse' and -delta rows, straight into their LDS slots (workgroup-uniform by wave)
+            lds_dma4(nl2 + qb, lds_addr32(&sl[buf][0]));
+            lds_dma4(nd + qb, lds_addr32(&sd[buf][0]));
         }
     };
     auto store_rows2 = [&](int buf) {
@@ -837,16 +851,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 32 ? DK
         // fp64: 7.2e-3 vs 4.0e-3 rel L2, bf16 at L 4096; profiles/r05/attn_prescale). dK's product reads the same
         // image and is rescaled by scale / c at the end (a second, unscaled Q image cost +15 % dK,dV time; scaling
         // the staged tile here +8.5 %)
-        if constexpr (DMA) vm_wait();  // this wave's copies landed (the barrier publishes every wave's)
-        else ld_.store(Qs[buf], Os[buf], LDK);
-        if (tid < 64) {  // stored negated: the accumulator inits
-            // (the row index recomputed here: the two LDS addresses hoisted out of the query loop were spilled at the
-            // 128-VGPR cap, and their scratch reloads sat on wave 0's path to every tile's barrier)
-            int row = tid;
-            asm volatile("" : "+v"(row));
-            sl[buf][row] = -pl;
-            sd[buf][row] = -pd;
-        }
+        if constexpr (!DMA) ld_.store(Qs[buf], Os[buf], LDK);
+        vm_wait();  // this wave's copies landed (the barrier publishes every wave's)
     };
     load_rows2(0, 0);
     store_rows2(0);
@@ -948,7 +954,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
                                                  const typename Ty<DT>::T *__restrict__ k,
                                                  const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                  const typename Ty<DT>::T *__restrict__ dout,
-                                                 const float *__restrict__ lse, float *__restrict__ delta,
+                                                 const float *__restrict__ lse, float *__restrict__ nrow,
                                                  typename Ty<DT>::T *__restrict__ dq, long long ldd,
                                                  const typename Ty<DT>::T *__restrict__ o,
                                                  typename Ty<DT>::T *__restrict__ qc) {
@@ -975,7 +981,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
         l2[s] = qv ? lse[(long long)bh * L + qr] * LOG2E : INFINITY;
         // delta = rowsum(dO o O) of this lane's row, here instead of a separate pass: each of the row's four lanes
         // (g) holds D / 4 of its elements; their partial sums meet by two lane exchanges, and lane g = 0 stores the
-        // row's delta for k_attn_dkdv2 (launched after this kernel)
+        // row's -delta and -lse' for k_attn_dkdv2 (launched after this kernel; row_pitch)
         {
             YFrag<DT, D> ofr;
             load_yfrag<DT, D>(ofr, o + obase + (long long)qr * H * D, qv, g);
@@ -987,7 +993,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? BW
             part += __shfl_xor(part, 16, 64);
             part += __shfl_xor(part, 32, 64);
             dl[s] = qv ? part : 0.f;
-            if (qv && g == 0) delta[(long long)bh * L + qr] = part;
+            const int Lp = row_pitch(L);
+            if (g == 0 && qr < Lp) {  // (the grid covers every row below Lp: 64 QS rows per workgroup)
+                nrow[(long long)bh * Lp + qr] = qv ? -l2[s] : -INFINITY;
+                nrow[(long long)gridDim.y * Lp + (long long)bh * Lp + qr] = qv ? -part : 0.f;
+            }
         }
         prescale<DT, D / 32>(qf[s].v, c);  // S in log2 units
         if (qv) {  // the rounded Q * c rows for k_attn_dkdv2 ([B*H][L][D]), so it recomputes this P exactly
@@ -1128,8 +1138,11 @@ int fwd_impl(int B, int L, int H, float scale, const void *q, const void *k, con
     return LGM_OK;
 }
 
-// backward workspace: delta [B*H][L] fp32, then (16-bit types) Q * scale * log2(e) [B*H][L][D] in the input type
-size_t qc_offset(int B, int L, int H) { return ((size_t)B * L * H * sizeof(float) + 255) & ~(size_t)255; }
+// backward workspace. fp32: delta [B*H][L]. 16-bit: -lse' and -delta [2][B*H][row_pitch(L)] fp32, then
+// Q * scale * log2(e) [B*H][L][D] in the input type.
+size_t qc_offset(int B, int L, int H) {
+    return (2 * (size_t)B * H * row_pitch(L) * sizeof(float) + 255) & ~(size_t)255;
+}
 
 template <int DT, int D>
 int bwd_impl(int B, int L, int H, float scale, const void *q, const void *k, const void *v, long long ld,
@@ -1146,12 +1159,12 @@ int bwd_impl(int B, int L, int H, float scale, const void *q, const void *k, con
             LGM_LAUNCH("k_attn_dq", st, (k_attn_dq2<DT, D, S2><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
                        (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd, (const T *)o, qc)));
             LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, S2><<<g2, NT, 0, st>>>(L, H, scale, (const T *)qc,
-                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dk, (T *)dv, ldd)));
+                       (const T *)k, (const T *)v, ld, (const T *)dout, delta, (T *)dk, (T *)dv, ldd)));
         } else {
             LGM_LAUNCH("k_attn_dq", st, (k_attn_dq2<DT, D, 1><<<g2, NT, 0, st>>>(L, H, scale, (const T *)q,
                        (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dq, ldd, (const T *)o, qc)));
             LGM_LAUNCH("k_attn_dkdv", st, (k_attn_dkdv2<DT, D, 1><<<g2, NT, 0, st>>>(L, H, scale, (const T *)qc,
-                       (const T *)k, (const T *)v, ld, (const T *)dout, lse, delta, (T *)dk, (T *)dv, ldd)));
+                       (const T *)k, (const T *)v, ld, (const T *)dout, delta, (T *)dk, (T *)dv, ldd)));
         }
         return LGM_OK;
     }
@@ -1198,7 +1211,7 @@ extern "C" {
 size_t lgm_attn_workspace_size(int dtype, int B, int L, int H, int D) {
     if (B <= 0 || L <= 0 || H <= 0 || D <= 0) return 0;
     if (dtype == LGM_ATTN_F32) return (size_t)B * L * H * sizeof(float);  // delta
-    return lgm::attn::qc_offset(B, L, H) + (size_t)B * L * H * D * 2;      // delta, Q * c
+    return lgm::attn::qc_offset(B, L, H) + (size_t)B * L * H * D * 2;      // row constants, Q * c
 }
 
 int lgm_attn_forward(int dtype, int B, int L, int H, int D, float scale, const void *q, const void *k,

@@ -245,6 +245,43 @@ def test_packed_attention_vs_fp64(cuda, shape, dtype, tol):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("jump", [6.0, 30.0, 100.0, -100.0])
+@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 2e-2), (torch.float16, 3e-3)], ids=["bf16", "f16"])
+@pytest.mark.parametrize("D", [32, 64])
+def test_forward_score_jump(cuda, D, dtype, tol, jump):
+    """The forward's online softmax where one key of a LATER key tile scores `jump` (log2 units) above every key of
+    the first tile, for every query (or, negative, far below): the paths that raise the row reference m mid-row
+    (rare on bounded random data, so pinned here) must give the fp64 result. Gradients at 2x the bar: with a
+    near-one-hot softmax dS = P (dP - delta) is a cancellation, which amplifies the 16-bit rounding of the recomputed
+    P (f16, jump 30: dq 5.0e-3 for this kernel)."""
+    from lgm_amd.attention import packed_attention
+    B, L, H = 1, 320, 2
+    scale = D ** -0.5
+    g = torch.Generator(device="cpu").manual_seed(int(abs(jump)) * 13 + D + (1 if jump < 0 else 0))
+    c = torch.full((D,), 0.5)
+    qkv = torch.randn((B, L, 3, H, D), generator=g) * 0.3
+    qkv[:, :, 0] += c  # every query ~ c
+    # key 200 (the fourth 64-key tile) scores ~ jump (log2 units) above the others for every query
+    beta = jump / (1.4426950408889634 * scale * float(c @ c))
+    qkv[:, 200, 1] = beta * c
+    qkv = qkv.to(cuda, dtype)
+    d_o = torch.randn((B, L, H, D), generator=g).to(cuda, dtype)
+    x = qkv.clone().requires_grad_(True)
+    o = packed_attention(x, scale)
+    o.backward(d_o)
+    o = o.detach()
+    torch.cuda.synchronize()
+    o_t, dqkv_t = _packed_truth(qkv, scale, d_o)
+    assert torch.isfinite(o).all() and torch.isfinite(x.grad).all()
+    assert rel_l2(o.double().cpu().numpy(), o_t.cpu().numpy()) < tol
+    floor = 1e-2 * float(dqkv_t.norm())
+    for i, name in enumerate("qkv"):
+        a, b = x.grad[:, :, i].double(), dqkv_t[:, :, i]
+        err = float((a - b).norm()) / max(float(b.norm()), floor)
+        assert err < 2 * tol, (name, err)
+
+
+@pytest.mark.gpu
 def test_memory_efficient_attention_views_and_copies(cuda):
     """xformers-style entry: unbind views of the packed tensor run in place; unrelated q/k/v are stacked."""
     from lgm_amd.attention import memory_efficient_attention

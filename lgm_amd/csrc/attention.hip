@@ -561,6 +561,10 @@ constexpr int LDK_PAD = 16, FWD_WPE = 3, BWD_WPE = 2;
 // VGPRs; 3 at the compiler's own 136): bench level k_attn_dkdv 636 -> 625 us (profiles/r04/ab_session_f; the
 // forward split the same way ran 412 -> 435 us and stays whole)
 constexpr int DKDV_WPE32 = 4;
+// The two-sub-tile forward at D = 32 (grids of 512 .. 1,535 workgroups, e.g. cfg4's L = 9,600 level at 1,200) held
+// at 5 waves per SIMD (96 VGPRs, spills outside the key loop only): 1,280 workgroup slots hold the whole grid in one
+// round (4 waves: 1,024 slots, 1.17 rounds): cfg4 L = 9,600 k_attn_fwd 268.4 -> 264.2 us (profiles/r05/ab_attn_q2w5)
+constexpr int FWD_WPE_Q2 = 5;
 // The softmax's affine parts ride on the MFMAs: Q is pre-scaled by scale * log2(e) (rounded to the 16-bit type once;
 // in registers in the forward and dQ kernels, as a second LDS image in dK/dV -- all three recompute P from the same
 // rounded operands), so S comes out in log2 units, and the S / dP
@@ -598,7 +602,7 @@ __device__ __forceinline__ void tile_loop(int L, Step &&step) {
     }
 }
 template <int DT, int D, int QS>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D <= 64 ? FWD_WPE : 1))) void k_attn_fwd2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(D == 32 && QS == 2 ? FWD_WPE_Q2 : D <= 64 ? FWD_WPE : 1))) void k_attn_fwd2(int L, int H, float scale, const typename Ty<DT>::T *__restrict__ q,
                                                   const typename Ty<DT>::T *__restrict__ k,
                                                   const typename Ty<DT>::T *__restrict__ v, long long ld,
                                                   typename Ty<DT>::T *__restrict__ o, float *__restrict__ lse) {

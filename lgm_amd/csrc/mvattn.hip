@@ -1,9 +1,9 @@
 // lgm_amd/csrc/mvattn.hip -- the token layout changes around MVAttention's attention core (core/unet.py:35-49),
 // fused with the GroupNorm before and the residual after:
-//   k_mva_stats + k_mva_norm   GroupNorm(x) of [B*F, C, H, W] (core/unet.py:40, fp32 statistics), written
-//                straight into the [B, F*H*W, C] token layout of :41-42 in the qkv Linear's input dtype (bf16 under
-//                autocast): two launches instead of torch's moments / fused-params / normalise launches + the
-//                permute copy + the cast.
+//   k_mva_gn_tok (or, for slabs beyond LDS, k_mva_stats + k_mva_norm)   GroupNorm(x) of [B*F, C, H, W]
+//                (core/unet.py:40, fp32 statistics), written straight into the [B, F*H*W, C] token layout of :41-42
+//                in the qkv Linear's input dtype (bf16 under autocast): one launch instead of torch's moments /
+//                fused-params / normalise launches + the permute copy + the cast.
 //   k_mva_out    the [B, F*H*W, C] -> [B*F, C, H, W] permute of :45-46 fused with (x + res) * skip_scale of :47-48.
 // Both are HBM-bound layout kernels: 64x64 LDS-tiled transposes, so global reads and writes run along rows.
 #include <hip/hip_bf16.h>
@@ -125,6 +125,93 @@ __global__ __launch_bounds__(256) void k_mva_norm(int F, int C, int HW, int G, f
     for (int k = 0; k < 16; k++) {
         const int i = tid + 256 * k, r = i >> 6, c = i & 63;  // token row r, channel c
         if (hw0 + r < HW && c0 + c < C) tb[(size_t)(hw0 + r) * C + c0 + c] = from_f<TO>(tile[r][c]);
+    }
+}
+
+// k_mva_gn_tok  grid (G, B*F), block 512: the same GroupNorm -> tokens in ONE launch where a group's Cg x HW slab
+//               fits in LDS (every LGM level: <= 100 KB): the slab is read once into LDS (float4 loads for fp32
+//               input), its mean and centred sum of squares reduced in a fixed order (two passes over LDS), then
+//               written normalised along the token rows (Cg / 8 x 16-B stores per token). Replaces the chunked
+//               statistics launch + the tiled normalise launch (their fixed launch latency dominated LGM's small
+//               levels: 600 and 2,400 tokens at C = 1024). cfg4's 16 blocks: GPU span per pass 2.43 -> 2.38 ms
+//               (profiles/r05/ab_mva_gn_fused).
+constexpr int GN_THREADS = 512;
+constexpr size_t GN_LDS_MAX = 144 * 1024;  // bytes of dynamic LDS the fused form may take
+
+__device__ __forceinline__ float block_sum512(float v, float *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();  // red is reused between calls
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));  // fixed order
+}
+
+template <class TI, class TO>
+__global__ __launch_bounds__(GN_THREADS) void k_mva_gn_tok(int F, int C, int HW, int G, float eps,
+                                                            const TI *__restrict__ x, const float *__restrict__ gamma,
+                                                            const float *__restrict__ beta, TO *__restrict__ tok,
+                                                            float *__restrict__ mean_out, float *__restrict__ rstd_out) {
+    extern __shared__ __attribute__((aligned(16))) float slab[];  // [Cg][HW], then a[Cg], b[Cg]
+    __shared__ float red[8];
+    const int g = blockIdx.x, bf = blockIdx.y, Cg = C / G, n = Cg * HW, tid = threadIdx.x;
+    const TI *xg = x + ((size_t)bf * C + (size_t)g * Cg) * HW;
+    float s = 0.f;
+    if constexpr (sizeof(TI) == 4) {
+        if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
+            const float4 *x4 = reinterpret_cast<const float4 *>(xg);
+            for (int i = tid; i < n / 4; i += GN_THREADS) {
+                const float4 v = x4[i];
+                reinterpret_cast<float4 *>(slab)[i] = v;
+                s += (v.x + v.y) + (v.z + v.w);
+            }
+        } else {
+            for (int i = tid; i < n; i += GN_THREADS) { const float v = to_f(xg[i]); slab[i] = v; s += v; }
+        }
+    } else {
+        for (int i = tid; i < n; i += GN_THREADS) { const float v = to_f(xg[i]); slab[i] = v; s += v; }
+    }
+    const float mean = block_sum512(s, red) / (float)n;
+    float q = 0.f;
+    for (int i = tid; i < n; i += GN_THREADS) {
+        const float d = slab[i] - mean;
+        q = fmaf(d, d, q);
+    }
+    const float rstd = rsqrtf(block_sum512(q, red) / (float)n + eps);  // biased variance, as torch
+    float *sa = slab + n, *sb = sa + Cg;
+    for (int c = tid; c < Cg; c += GN_THREADS) {
+        const float a = rstd * (gamma ? gamma[g * Cg + c] : 1.f);
+        sa[c] = a;
+        sb[c] = (beta ? beta[g * Cg + c] : 0.f) - mean * a;
+    }
+    if (tid == 0) {
+        mean_out[(size_t)bf * G + g] = mean;
+        rstd_out[(size_t)bf * G + g] = rstd;
+    }
+    __syncthreads();
+    const int b = bf / F, f = bf - b * F;
+    TO *tb = tok + ((size_t)b * F * HW + (size_t)f * HW) * C + (size_t)g * Cg;
+    if ((Cg & 7) == 0) {  // 8 channels per thread: one 16-B (bf16) / 32-B (fp32) store
+        const int c8n = Cg / 8;
+        for (int p = tid; p < HW * c8n; p += GN_THREADS) {
+            const int hw = p / c8n, c0 = (p - hw * c8n) * 8;
+            TO o[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) o[j] = from_f<TO>(fmaf(slab[(c0 + j) * HW + hw], sa[c0 + j], sb[c0 + j]));
+            TO *dst = tb + (size_t)hw * C + c0;
+            if constexpr (sizeof(TO) == 2) {
+                *reinterpret_cast<uint4 *>(dst) = *reinterpret_cast<const uint4 *>(o);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++) dst[j] = o[j];
+            }
+        }
+    } else {
+        for (int p = tid; p < HW * Cg; p += GN_THREADS) {
+            const int hw = p / Cg, c = p - hw * Cg;
+            tb[(size_t)hw * C + c] = from_f<TO>(fmaf(slab[c * HW + hw], sa[c], sb[c]));
+        }
     }
 }
 
@@ -375,7 +462,22 @@ __global__ __launch_bounds__(256) void k_mva_gn_dx(int F, int C, int HW, int G, 
 template <class TI, class TO>
 int launch_norm(int B, int F, int C, int HW, int G, float eps, const void *x, const float *gamma, const float *beta,
                 void *tok, float *mean, float *rstd, float2 *part, hipStream_t st) {
-    const int S = (C / G * HW + MVA_CHUNK - 1) / MVA_CHUNK;
+    const size_t lds = ((size_t)(C / G) * HW + 2 * (C / G)) * sizeof(float);
+    if (lds <= GN_LDS_MAX) {  // one launch: the group's slab in LDS
+        static bool attr_set = false;  // (the kernel's dynamic LDS limit raised once per instantiation)
+        if (!attr_set) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mva_gn_tok<TI, TO>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)GN_LDS_MAX) != hipSuccess) {
+                set_error("hipFuncSetAttribute(k_mva_gn_tok) failed");
+                return LGM_E_HIP;
+            }
+            attr_set = true;
+        }
+        LGM_LAUNCH("k_mva_gn_tok", st, (k_mva_gn_tok<TI, TO><<<dim3(G, B * F), GN_THREADS, lds, st>>>(
+                                           F, C, HW, G, eps, (const TI *)x, gamma, beta, (TO *)tok, mean, rstd)));
+        return LGM_OK;
+    }
+    const int S = (C / G * HW + MVA_CHUNK - 1) / MVA_CHUNK;  // larger slabs: chunked statistics + tiled normalise
     LGM_LAUNCH("k_mva_stats", st,
                (k_mva_stats<TI><<<dim3(S, G, B * F), 256, 0, st>>>(C, HW, G, (const TI *)x, part)));
     const dim3 grid((HW + 63) / 64, (C + 63) / 64, B * F);

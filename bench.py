@@ -65,9 +65,10 @@ N_SIMD, CLK_HZ = 256 * 4, 2.4e9  # MI355X: 256 CUs x 4 SIMDs; peak engine clock
 def limiter_from_counters(rec, achieved_counter_gbs, avg_s=None):
     """What bounds a kernel, read off its PMC record (profiles/pmc_latest.json): HBM if the counted traffic runs at
     >= 60 % of peak; VALU issue if its VALU instructions fill >= 70 % of the chip's SIMD issue cycles over the
-    launch (a wave64 VALU instruction holds its SIMD's vector issue for 4 cycles: MI355X_MICROARCH's issue-cost row,
-    v_add / v_fma / v_max3 4, transcendentals 8; counted at 4 and at the peak clock, so a lower bound); else latency /
-    issue (the waves wait: barriers, LDS and memory round trips)."""
+    launch at 2 cycles per wave64 instruction (a lower bound: MI355X_MICROARCH prices one wave's stream at 4, but
+    across co-resident waves the SIMDs sustain more -- k_render_fwd's counted VALU at 4 cycles would need a 2.8 GHz
+    clock -- so the 4-cycle figure, reported beside it, is an upper bound); else latency / issue (the waves wait:
+    barriers, LDS and memory round trips)."""
     if not rec:
         return None
     hbm = achieved_counter_gbs / PEAK_HBM_GBS if achieved_counter_gbs else 0.0
@@ -75,9 +76,10 @@ def limiter_from_counters(rec, achieved_counter_gbs, avg_s=None):
     lds = rec.get("lds_bank_conflict_frac")
     issue = None
     if avg_s and rec.get("SQ_INSTS_VALU"):
-        issue = round(4.0 * rec["SQ_INSTS_VALU"] / (N_SIMD * avg_s * CLK_HZ), 4)
+        issue = round(2.0 * rec["SQ_INSTS_VALU"] / (N_SIMD * avg_s * CLK_HZ), 4)
     kind = "hbm" if hbm >= 0.6 else "valu-issue" if (issue or 0.0) >= 0.7 else "latency/issue"
     return {"kind": kind, "hbm_frac_at_counter_bytes": round(hbm, 4), "valu_issue_frac": issue,
+            "valu_issue_frac_at_4_cycles": round(2 * issue, 4) if issue is not None else None,
             "valu_busy_frac_per_wave": valu, "wait_frac": wait, "lds_bank_conflict_frac": lds}
 
 

@@ -130,7 +130,7 @@ int lgm_render_needle_flags(long long n, const float *abc, unsigned char *flags_
  * (room for B*V*ceil(N/512); the binning launch uses its first B*ceil(V/3)*ceil(N/512)): phase stamps [0] start,
  * [1] preprocessed, [2] tile tests done, [3] reserved, [4] end, [5] its binned pairs, [6] HW_ID and [7] XCC_ID of where it
  * ran; then 4 entries per backward work item (at most 3*B*V*tiles + 16 items: one per tile, rounded up to 8, and
- * one per checkpoint slot): start/end stamps, (entries | chunk << 20 | tile << 40) and one unused -- so the buffer
+ * one per checkpoint slot): start/end stamps, (entries | chunk << 20 | tile << 40) and (XCC_ID | HW_ID << 8) -- so the buffer
  * must hold 8 + 8*B*V*tiles + 8*B*V*ceil(N/512) + 4*(3*B*V*tiles + 16) entries. */
 
 /* Per-call `options` of lgm_render_forward / lgm_render_backward (pass the same value to both).

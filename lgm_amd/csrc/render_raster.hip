@@ -1187,6 +1187,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         o[0] = t_item;
         o[1] = __builtin_amdgcn_s_memrealtime();
         o[2] = (unsigned long long)(s1 - s0) | ((unsigned long long)c << 20) | ((unsigned long long)tile << 40);
+        o[3] = (unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) |        // XCC_ID (the XCD)
+               ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 8);  // HW_ID
     }
 }
 

@@ -3,7 +3,7 @@
 # (scripts/gpu_prof.sh), then bench.py unprofiled: twice with the defaults, once with the driver's arguments.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/final
-bash scripts/gpu_prof.sh || exit $?
+PMC_COMMIT=${PMC_COMMIT:-unknown} bash scripts/gpu_prof.sh || exit $?
 python scripts/kernel_stats_by_grid.py gpurun_out/prof/run_kernel_trace.csv > gpurun_out/prof/kernel_stats_by_grid.txt
 for r in 1 2; do
   timeout -k 10 400 python bench.py > gpurun_out/final/bench_plain$r.json 2> gpurun_out/final/bench_plain$r.err || exit $?

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round-5 session AD: k_render_bwd work order with each XCD's checkpoint items (full chunks of the long tiles) ahead of
+# its head items (lib_ckf) against heads first (lib_base): render GPU tests on ckf, scripts/diag_cu.py per library,
+# then bench.py pool + single scene, two interleaved rounds.
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/r5ad
+V=$PWD/lgm_amd/_lib/variants
+LGM_AMD_LIB=$V/lib_ckf.so timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_render_cases.py tests/test_render_gpu.py tests/test_render_parity_gpu.py -m gpu > gpurun_out/r5ad/t_ckf.log 2>&1
+rc=$?; echo "ckf tests: $(tail -1 gpurun_out/r5ad/t_ckf.log)"; [ $rc -eq 0 ] || exit $rc
+for n in base ckf; do
+  LGM_AMD_LIB=$V/lib_$n.so timeout -k 10 240 python scripts/diag_cu.py > gpurun_out/r5ad/cu_$n.json 2> gpurun_out/r5ad/cu_$n.err || exit $?
+done
+for round in 1 2; do
+  for n in base ckf; do
+    LGM_AMD_LIB=$V/lib_$n.so timeout -k 10 300 python bench.py --steps 40 --warmup 10 --no-cfg4 --no-cfg5 --no-attention --no-cpu-baseline --no-det > gpurun_out/r5ad/b_${n}_r${round}.json 2> gpurun_out/r5ad/b_${n}_r${round}.err || exit $?
+    python -c "
+import json
+b=json.load(open('gpurun_out/r5ad/b_${n}_r${round}.json')); c=b['cfg3_view_sharded']
+print('$n r$round pool', b['ms_per_step'], {k: v['avg_us'] for k, v in b['kernels'].items()}, 'cfg3', c['ms_per_step'], {k: v['avg_us'] for k, v in c['kernels'].items()})"
+  done
+done

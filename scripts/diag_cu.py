@@ -79,5 +79,15 @@ for rep in range(3):
     it = it[it[:, 1] > 0]
     bkey = (it[:, 3] & 0xFF) * 256 + ((it[:, 3] >> 16) & 0xFF)
     blen = it[:, 2] & 0xFFFFF
-    res[f"rep{rep}"] = {"fwd": per_cu(fkey, st, en, nl), "bwd": per_cu(bkey, it[:, 0], it[:, 1], blen)}
+    c_list, c_iter = tl[:, 7] & 0xFFFFFFFF, (tl[:, 7] >> 32) & 0xFFFFFF
+    dur = (en - st) * 0.01
+    top = np.argsort(-dur)[:6]
+    res[f"rep{rep}"] = {"fwd": per_cu(fkey, st, en, nl), "bwd": per_cu(bkey, it[:, 0], it[:, 1], blen),
+                        "fwd_longest [tile, us, list, staged, wave0_steps, start_us]": [
+                            [int(t), round(float(dur[t]), 2), int(nl[t]), int(c_list[t]), int(c_iter[t]),
+                             round(float((st[t] - st.min()) * 0.01), 2)] for t in top]}
+    if rep == 0:  # per-tile raw record of one run: CU key, start / end (us), list, staged, wave-0 entries
+        res["tiles_rep0 [cu_key, start_us, end_us, list, staged, wave0_entries]"] = [
+            [int(fkey[t]), round(float((st[t] - st.min()) * 0.01), 2), round(float((en[t] - st.min()) * 0.01), 2),
+             int(nl[t]), int(c_list[t]), int(c_iter[t])] for t in range(M)]
 print(json.dumps(res))

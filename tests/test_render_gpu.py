@@ -65,7 +65,8 @@ def _check_bwd(out, ref, tol=BWD_TOL):
 
 @pytest.mark.parametrize("B,N,V,H,W,mod", [(1, 1, 1, 32, 32, 1.0), (1, 300, 2, 64, 64, 1.0), (2, 2000, 3, 64, 64, 1.0),
                                            (1, 3000, 2, 50, 50, 0.7), (1, 2500, 2, 40, 72, 1.0),
-                                           (2, 1500, 2, 128, 128, 1.3)])
+                                           (2, 1500, 2, 128, 128, 1.3),
+                                           (1, 400, 34, 32, 32, 1.0)])  # > PRE_MAXV views: k_preproc_bwd<false>
 def test_forward_backward_parity(cuda, oracle_mod, B, N, V, H, W, mod):
     g, cv, cvp = scene(B=B, N=N, V=V, seed=N + V)
     grads = upstream(B, V, H, W)

@@ -134,7 +134,9 @@ __global__ __launch_bounds__(256) void k_mva_norm(int F, int C, int HW, int G, f
 //               written normalised along the token rows (Cg / 8 x 16-B stores per token). Replaces the chunked
 //               statistics launch + the tiled normalise launch (their fixed launch latency dominated LGM's small
 //               levels: 600 and 2,400 tokens at C = 1024). cfg4's 16 blocks: GPU span per pass 2.43 -> 2.38 ms
-//               (profiles/r05/ab_mva_gn_fused).
+//               (profiles/r05/ab_mva_gn_fused). The slab loads go 8 per thread at a time (the plain loop waited for
+//               each before issuing the next): bench level 34.2 -> 32.2 us, cfg4 190.8 -> 182.9 us per pass
+//               (profiles/r05/ab_mva_batch); the same for k_mva_gn_coef's tile partials (13.8 -> 11.5 us).
 constexpr int GN_THREADS = 512;
 constexpr size_t GN_LDS_MAX = 144 * 1024;  // bytes of dynamic LDS the fused form may take
 
@@ -161,7 +163,20 @@ __global__ __launch_bounds__(GN_THREADS) void k_mva_gn_tok(int F, int C, int HW,
     if constexpr (sizeof(TI) == 4) {
         if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
             const float4 *x4 = reinterpret_cast<const float4 *>(xg);
-            for (int i = tid; i < n / 4; i += GN_THREADS) {
+            int i = tid;
+            // 8 loads in flight per thread, then their LDS stores and sums in the same order (the plain loop waited
+            // for each load before issuing the next)
+            for (; i + 7 * GN_THREADS < n / 4; i += 8 * GN_THREADS) {
+                float4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = x4[i + u * GN_THREADS];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    reinterpret_cast<float4 *>(slab)[i + u * GN_THREADS] = v[u];
+                    s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+                }
+            }
+            for (; i < n / 4; i += GN_THREADS) {
                 const float4 v = x4[i];
                 reinterpret_cast<float4 *>(slab)[i] = v;
                 s += (v.x + v.y) + (v.z + v.w);
@@ -170,7 +185,18 @@ __global__ __launch_bounds__(GN_THREADS) void k_mva_gn_tok(int F, int C, int HW,
             for (int i = tid; i < n; i += GN_THREADS) { const float v = to_f(xg[i]); slab[i] = v; s += v; }
         }
     } else {
-        for (int i = tid; i < n; i += GN_THREADS) { const float v = to_f(xg[i]); slab[i] = v; s += v; }
+        int i = tid;
+        for (; i + 7 * GN_THREADS < n; i += 8 * GN_THREADS) {  // (as above, 16-bit elements)
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = to_f(xg[i + u * GN_THREADS]);
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                slab[i + u * GN_THREADS] = v[u];
+                s += v[u];
+            }
+        }
+        for (; i < n; i += GN_THREADS) { const float v = to_f(xg[i]); slab[i] = v; s += v; }
     }
     const float mean = block_sum512(s, red) / (float)n;
     float q = 0.f;
@@ -385,7 +411,18 @@ __global__ __launch_bounds__(256) void k_mva_gn_coef(int BF, int C, int HW, int 
             const int n = n0 + it / Cg, c = g * Cg + it % Cg;
             const float2 *pp = part + ((size_t)n * C + c) * nT;
             float a = 0.f, b = 0.f;
-            for (int t = 0; t < nT; t++) {  // fixed order over the pixel tiles
+            int t = 0;
+            for (; t + 8 <= nT; t += 8) {  // 8 loads in flight, then the sums in the same fixed order
+                float2 p[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) p[u] = pp[t + u];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    a += p[u].x;
+                    b += p[u].y;
+                }
+            }
+            for (; t < nT; t++) {  // fixed order over the pixel tiles
                 const float2 p = pp[t];
                 a += p.x;
                 b += p.y;

@@ -1,6 +1,7 @@
 // lgm_amd/csrc/mvattn.hip -- the token layout changes around MVAttention's attention core (core/unet.py:35-49),
 // fused with the GroupNorm before and the residual after:
-//   k_mva_gn_tok (or, for slabs beyond LDS, k_mva_stats + k_mva_norm)   GroupNorm(x) of [B*F, C, H, W]
+//   k_mva_gn_reg (slab in registers; else k_mva_gn_tok with the slab in LDS, or for slabs beyond LDS k_mva_stats +
+//   k_mva_norm)  GroupNorm(x) of [B*F, C, H, W]
 //                (core/unet.py:40, fp32 statistics), written straight into the [B, F*H*W, C] token layout of :41-42
 //                in the qkv Linear's input dtype (bf16 under autocast): one launch instead of torch's moments /
 //                fused-params / normalise launches + the permute copy + the cast.
@@ -237,6 +238,111 @@ __global__ __launch_bounds__(GN_THREADS) void k_mva_gn_tok(int F, int C, int HW,
         for (int p = tid; p < HW * Cg; p += GN_THREADS) {
             const int hw = p / Cg, c = p - hw * Cg;
             tb[(size_t)hw * C + c] = from_f<TO>(fmaf(slab[c * HW + hw], sa[c], sb[c]));
+        }
+    }
+}
+
+// k_mva_gn_reg  grid (G, B*F), block 512: the one-launch GroupNorm -> tokens with the group's slab in REGISTERS
+//               instead of LDS, for Cg % 8 == 0 channels, HW % 4 == 0 and <= GNR_K * 512 items (every LGM level). An
+//               item is 8 channel rows x 4 pixels: thread t holds items t + 512 k (channel block fastest, so the lanes
+//               of one pixel quad write adjacent 16 B of each token row), loaded as one 4-pixel vector per channel row,
+//               all in flight at once; the statistics are
+//               reduced in a fixed order (two passes over the registers); each pixel of an item is written as one
+//               token-row store of 8 channels. No LDS slab, so LDS does not cap the launch at two workgroups per CU.
+//               Against k_mva_gn_tok: bench level 31.8 -> 29.5 us, cfg4 184.4 -> 153.3 us per pass (its C = 512 level
+//               has 192 workgroups: all loads in flight at once matters most there; profiles/r05/ab_mva_gn_reg).
+constexpr int GNR_K = 2;  // items per thread (64 registers of slab)
+template <class TI>
+__device__ __forceinline__ void load4(const TI *p, float (&o)[4]) {
+    if constexpr (sizeof(TI) == 4) {
+        const float4 t = *reinterpret_cast<const float4 *>(p);
+        o[0] = t.x; o[1] = t.y; o[2] = t.z; o[3] = t.w;
+    } else {
+        const uint2 t = *reinterpret_cast<const uint2 *>(p);
+        TI e[4];
+        *reinterpret_cast<uint2 *>(e) = t;
+#pragma unroll
+        for (int j = 0; j < 4; j++) o[j] = to_f(e[j]);
+    }
+}
+template <class TI, class TO>
+__global__ __launch_bounds__(GN_THREADS) void k_mva_gn_reg(int F, int C, int HW, int G, float eps,
+                                                            const TI *__restrict__ x, const float *__restrict__ gamma,
+                                                            const float *__restrict__ beta, TO *__restrict__ tok,
+                                                            float *__restrict__ mean_out, float *__restrict__ rstd_out) {
+    __shared__ float red[8];
+    __shared__ float sab[2][256];  // per channel of the group: a = rstd gamma, b = beta - mean a (Cg <= 256)
+    const int g = blockIdx.x, bf = blockIdx.y, Cg = C / G, tid = threadIdx.x;
+    const int nCB = Cg / 8, nit = nCB * (HW / 4);  // items (channel block fastest: lane pairs share a pixel quad)
+    const TI *xg = x + ((size_t)bf * C + (size_t)g * Cg) * HW;
+    float v[GNR_K][8][4];
+#pragma unroll
+    for (int k = 0; k < GNR_K; k++) {
+        const int it = tid + GN_THREADS * k;
+        const int p4 = it / nCB, cb = it - p4 * nCB;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (it < nit) load4<TI>(xg + (size_t)(8 * cb + j) * HW + 4 * p4, v[k][j]);
+            else v[k][j][0] = v[k][j][1] = v[k][j][2] = v[k][j][3] = 0.f;
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < GNR_K; k++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) s += (v[k][j][0] + v[k][j][1]) + (v[k][j][2] + v[k][j][3]);  // (past nit: 0)
+    const float n = (float)Cg * (float)HW;
+    const float mean = block_sum512(s, red) / n;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < GNR_K; k++) {
+        if (tid + GN_THREADS * k < nit) {
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const float d = v[k][j][e] - mean;
+                    q = fmaf(d, d, q);
+                }
+        }
+    }
+    const float rstd = rsqrtf(block_sum512(q, red) / n + eps);  // biased variance, as torch
+    for (int c = tid; c < Cg; c += GN_THREADS) {
+        const float a = rstd * (gamma ? gamma[g * Cg + c] : 1.f);
+        sab[0][c] = a;
+        sab[1][c] = (beta ? beta[g * Cg + c] : 0.f) - mean * a;
+    }
+    if (tid == 0) {
+        mean_out[(size_t)bf * G + g] = mean;
+        rstd_out[(size_t)bf * G + g] = rstd;
+    }
+    __syncthreads();
+    const int b = bf / F, f = bf - b * F;
+    TO *tb = tok + ((size_t)b * F * HW + (size_t)f * HW) * C + (size_t)g * Cg;
+#pragma unroll
+    for (int k = 0; k < GNR_K; k++) {
+        const int it = tid + GN_THREADS * k;
+        if (it < nit) {
+            const int p4 = it / nCB, cb = it - p4 * nCB;
+            float a8[8], b8[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                a8[j] = sab[0][8 * cb + j];
+                b8[j] = sab[1][8 * cb + j];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                TO o[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) o[j] = from_f<TO>(fmaf(v[k][j][e], a8[j], b8[j]));
+                TO *dst = tb + (size_t)(4 * p4 + e) * C + 8 * cb;
+                if constexpr (sizeof(TO) == 2) {
+                    *reinterpret_cast<uint4 *>(dst) = *reinterpret_cast<const uint4 *>(o);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) dst[j] = o[j];
+                }
+            }
         }
     }
 }
@@ -499,6 +605,13 @@ __global__ __launch_bounds__(256) void k_mva_gn_dx(int F, int C, int HW, int G, 
 template <class TI, class TO>
 int launch_norm(int B, int F, int C, int HW, int G, float eps, const void *x, const float *gamma, const float *beta,
                 void *tok, float *mean, float *rstd, float2 *part, hipStream_t st) {
+    const int Cg = C / G;
+    if (Cg % 8 == 0 && Cg <= 256 && HW % 4 == 0 &&
+        (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (long long)(Cg / 8) * (HW / 4) <= (long long)GNR_K * GN_THREADS) {
+        LGM_LAUNCH("k_mva_gn_tok", st, (k_mva_gn_reg<TI, TO><<<dim3(G, B * F), GN_THREADS, 0, st>>>(
+                                           F, C, HW, G, eps, (const TI *)x, gamma, beta, (TO *)tok, mean, rstd)));
+        return LGM_OK;
+    }
     const size_t lds = ((size_t)(C / G) * HW + 2 * (C / G)) * sizeof(float);
     if (lds <= GN_LDS_MAX) {  // one launch: the group's slab in LDS
         static bool attr_set = false;  // (the kernel's dynamic LDS limit raised once per instantiation)

@@ -395,6 +395,93 @@ __global__ __launch_bounds__(256) void k_mva_out(int F, int C, int HW, const TY 
     }
 }
 
+template <class T>
+__device__ __forceinline__ void load8(const T *p, float (&o)[8]) {
+    if constexpr (sizeof(T) == 4) {
+        const float4 a = reinterpret_cast<const float4 *>(p)[0], b = reinterpret_cast<const float4 *>(p)[1];
+        o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+    } else {
+        T e[8];
+        *reinterpret_cast<uint4 *>(e) = *reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = to_f(e[j]);
+    }
+}
+template <class T>
+__device__ __forceinline__ void store4(T *p, const float (&v)[4]) {
+    if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+        T e[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) e[j] = from_f<T>(v[j]);
+        *reinterpret_cast<uint2 *>(p) = *reinterpret_cast<const uint2 *>(e);
+    }
+}
+// k_mva_out with vector accesses (C % 8 == 0, HW % 4 == 0, 16-B aligned tensors): the tokens read 8 channels per
+// lane (16 B at 16 bits), the residual read and the output written 4 pixels per lane; the residual's loads go out
+// with the tokens' (one round trip). Same arithmetic, bitwise equal. Against k_mva_out: bench level 37.0 -> 31.2 us,
+// cfg4 171.6 -> 141.0 us per pass (profiles/r05/ab_mva_vec).
+template <class TY, class TR, class TO>
+__global__ __launch_bounds__(256) void k_mva_out_v(int F, int C, int HW, const TY *__restrict__ y,
+                                                   const TR *__restrict__ res, float skip, TO *__restrict__ out) {
+    __shared__ float tile[64][65];
+    const int hw0 = blockIdx.x * 64, c0 = blockIdx.y * 64, bf = blockIdx.z, tid = threadIdx.x;
+    const int b = bf / F, f = bf - b * F;
+    const TY *yb = y + ((size_t)b * F * HW + (size_t)f * HW) * C;
+    float v[2][8], rv[4][4];
+    // every load unconditional, out-of-range lanes on a clamped in-range address (their values are never used), so
+    // all six go out before the first wait
+#pragma unroll
+    for (int k = 0; k < 2; k++) {  // token row r, channels 8 q .. 8 q + 7
+        const int i = tid + 256 * k, r = i >> 3, q = i & 7;
+        const bool ok = hw0 + r < HW && c0 + 8 * q < C;
+        load8<TY>(yb + (ok ? (size_t)(hw0 + r) * C + c0 + 8 * q : 0), v[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // channel row r, pixels 4 p .. 4 p + 3
+        const int i = tid + 256 * k, r = i >> 4, p = i & 15;
+        const bool ok = c0 + r < C && hw0 + 4 * p < HW;
+        if (res) {
+            const TR *src = res + (ok ? ((size_t)bf * C + c0 + r) * HW + hw0 + 4 * p : 0);
+            if constexpr (sizeof(TR) == 4) {
+                const float4 a = *reinterpret_cast<const float4 *>(src);
+                rv[k][0] = a.x; rv[k][1] = a.y; rv[k][2] = a.z; rv[k][3] = a.w;
+            } else {
+                TR e[4];
+                *reinterpret_cast<uint2 *>(e) = *reinterpret_cast<const uint2 *>(src);
+#pragma unroll
+                for (int j = 0; j < 4; j++) rv[k][j] = to_f(e[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int i = tid + 256 * k, r = i >> 3, q = i & 7;
+#pragma unroll
+        for (int j = 0; j < 8; j++) tile[8 * q + j][r] = v[k][j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = tid + 256 * k, r = i >> 4, p = i & 15;
+        if (c0 + r < C && hw0 + 4 * p < HW) {
+            float o4[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                float t = tile[r][4 * p + e];
+                if (res) {
+                    t += rv[k][e];
+                    t = to_f(from_f<TO>(t));  // (exact for an fp32 output)
+                    t *= skip;
+                }
+                o4[e] = t;
+            }
+            store4<TO>(out + ((size_t)bf * C + c0 + r) * HW + hw0 + 4 * p, o4);
+        }
+    }
+}
+
 // ---- backward (core/unet.py:40-48 backward), the mirror of the two passes above:
 // k_mva_out_bwd   grid (ceil(HW/64), ceil(C/64), B*F): g = dL/dout * scale (rounded to out's dtype, as torch's
 //                 `d_out * skip`), written to d_res [B*F, C, H, W] along hw and, through the 64 x 64 LDS tile, to the
@@ -639,6 +726,13 @@ int launch_norm(int B, int F, int C, int HW, int G, float eps, const void *x, co
 template <class TY, class TR, class TO>
 int launch_out(int B, int F, int C, int HW, const void *y, const void *res, float skip, void *out, hipStream_t st) {
     const dim3 grid((HW + 63) / 64, (C + 63) / 64, B * F);
+    const bool vec = C % 8 == 0 && HW % 4 == 0 && ((reinterpret_cast<uintptr_t>(y) |
+                     reinterpret_cast<uintptr_t>(res) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    if (vec) {
+        LGM_LAUNCH("k_mva_out", st, (k_mva_out_v<TY, TR, TO><<<grid, 256, 0, st>>>(F, C, HW, (const TY *)y,
+                                                                                  (const TR *)res, skip, (TO *)out)));
+        return LGM_OK;
+    }
     LGM_LAUNCH("k_mva_out", st,
                (k_mva_out<TY, TR, TO><<<grid, 256, 0, st>>>(F, C, HW, (const TY *)y, (const TR *)res, skip, (TO *)out)));
     return LGM_OK;

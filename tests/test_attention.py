@@ -158,7 +158,10 @@ def test_module_bf16_autocast(cuda, path):
 
 
 MVA_CASES = [  # C, heads, frames, H, W, batch -- LGM levels (D = 32 / 64) and ragged ones (Cg = 3: scalar stores)
-    (512, 16, 6, 16, 16, 1), (1024, 16, 6, 10, 10, 1), (256, 8, 4, 8, 8, 2), (96, 3, 2, 7, 5, 1)]
+    # the LGM-shaped cases run the register-slab GroupNorm and the vector-access layout kernels; (96, ..., 7, 5)
+    # their scalar forms (HW % 4 != 0, Cg % 8 != 0); 48 x 48 at Cg = 16 the LDS-slab GroupNorm (> 1,024 items)
+    (512, 16, 6, 16, 16, 1), (1024, 16, 6, 10, 10, 1), (256, 8, 4, 8, 8, 2), (96, 3, 2, 7, 5, 1),
+    (512, 16, 1, 48, 48, 1)]
 
 
 @pytest.mark.gpu

@@ -118,6 +118,13 @@ int lgm_render_records(int B, int V, int N, int H, int W, const void *workspace,
  * flags_out [n] (DEVICE u8, 1 = needle). The binning and the backward's flush take this same decision on the stored
  * record; a test pins it to separately rounded IEEE operations (no FP contraction) near the threshold. */
 int lgm_render_needle_flags(long long n, const float *abc, unsigned char *flags_out, void *stream);
+/* lgm_render_det_flush_limit_log2: LGM_RENDER_DETERMINISTIC's overflow bound, log2 of the largest |flush| (in
+ * fixed-point units) the backward accepts into one int64 accumulator of a render with `views` views per scene and
+ * `tiles` tiles per view: 62 - ceil(log2 F), F = the flushes one accumulator can take -- `tiles` for the per-view
+ * records (mean2D, conic, depth), views * tiles for the per-scene ones (scene_record != 0: opacity, colour, summed
+ * over the scene's views). Pure host function (no GPU); the kernel derives the same value. A flush above it is
+ * counted and the call's gradients are poisoned with NaN. */
+int lgm_render_det_flush_limit_log2(int views, int tiles, int scene_record);
 
 /* Diagnostics: when diag->render_counters (a DEVICE uint64 buffer, caller-zeroed) is set, that call's render kernels
  * record per-workgroup timelines in it: [0..7] the backward's section cycles in the LGM_BWD_STAMPS diagnostic build (else unused);

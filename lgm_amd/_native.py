@@ -58,6 +58,7 @@ SIGNATURES = {
     "lgm_render_pixel_state": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp]),
     "lgm_render_records": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_size, _c_ll, _vp, _vp, _vp, _vp]),
     "lgm_render_needle_flags": (_c_int, [_c_ll, _vp, _vp, _vp]),
+    "lgm_render_det_flush_limit_log2": (_c_int, [_c_int, _c_int, _c_int]),
     "lgm_gaussian_head_forward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp,
                                            _c_size, _vp, _vp]),
     "lgm_gaussian_head_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),

@@ -589,6 +589,7 @@ __global__ __launch_bounds__(256) void k_mva_gn_part(int F, int C, int HW, const
 }
 
 constexpr int GN_NMAX = 2048;  // (sample, channel) pairs of one group held in LDS at a time
+constexpr int GN_CPT = GN_NMAX / 256;  // channels per thread of k_mva_gn_coef (any Cg <= GN_NMAX)
 __global__ __launch_bounds__(256) void k_mva_gn_coef(int BF, int C, int HW, int G, int nT,
                                                      const float2 *__restrict__ part, const float *__restrict__ gamma,
                                                      const float *__restrict__ mean, const float *__restrict__ rstd,
@@ -598,7 +599,10 @@ __global__ __launch_bounds__(256) void k_mva_gn_coef(int BF, int C, int HW, int 
     const int g = blockIdx.x, Cg = C / G, tid = threadIdx.x;
     const float s = 1.f / ((float)Cg * (float)HW);
     const int nchunk = max(1, GN_NMAX / Cg);  // samples per LDS chunk
-    float dg = 0.f, dbt = 0.f;                // this thread's channel (tid < Cg), summed over the samples in order
+    // this thread's channels tid + 256 k (k < GN_CPT, Cg <= GN_NMAX), each summed over the samples in order
+    float dg[GN_CPT], dbt[GN_CPT];
+#pragma unroll
+    for (int k = 0; k < GN_CPT; k++) dg[k] = dbt[k] = 0.f;
     for (int n0 = 0; n0 < BF; n0 += nchunk) {
         const int n1 = min(BF, n0 + nchunk), items = (n1 - n0) * Cg;
         for (int it = tid; it < items; it += 256) {
@@ -637,19 +641,27 @@ __global__ __launch_bounds__(256) void k_mva_gn_coef(int BF, int C, int HW, int 
             const float c3 = -c2 * mu - sum2 * rs * s;
             coef[(size_t)n * G + g] = make_float2(c2, c3);
         }
-        if (tid < Cg) {  // per channel: dgamma, dbeta over this chunk's samples, in order
-            for (int n = n0; n < n1; n++) {
-                const float2 v = sdb[(n - n0) * Cg + tid];
-                const float mu = mean[(size_t)n * G + g], rs = rstd[(size_t)n * G + g];
-                dg = fmaf(v.x - v.y * mu, rs, dg);
-                dbt += v.y;
+#pragma unroll
+        for (int k = 0; k < GN_CPT; k++) {  // per channel: dgamma, dbeta over this chunk's samples, in order
+            const int c = tid + 256 * k;
+            if (c < Cg) {
+                for (int n = n0; n < n1; n++) {
+                    const float2 v = sdb[(n - n0) * Cg + c];
+                    const float mu = mean[(size_t)n * G + g], rs = rstd[(size_t)n * G + g];
+                    dg[k] = fmaf(v.x - v.y * mu, rs, dg[k]);
+                    dbt[k] += v.y;
+                }
             }
         }
         __syncthreads();  // (sdb is rewritten by the next chunk)
     }
-    if (tid < Cg) {
-        if (dgamma) dgamma[g * Cg + tid] = dg;
-        if (dbeta) dbeta[g * Cg + tid] = dbt;
+#pragma unroll
+    for (int k = 0; k < GN_CPT; k++) {
+        const int c = tid + 256 * k;
+        if (c < Cg) {
+            if (dgamma) dgamma[g * Cg + c] = dg[k];
+            if (dbeta) dbeta[g * Cg + c] = dbt[k];
+        }
     }
 }
 
@@ -872,20 +884,19 @@ int launch_norm(int B, int F, int C, int HW, int G, float eps, const void *x, co
     const int Cg = C / G;
     if (Cg % 8 == 0 && Cg <= 256 && HW % 4 == 0 &&
         (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (long long)(Cg / 8) * (HW / 4) <= (long long)GNR_K * GN_THREADS) {
-        LGM_LAUNCH("k_mva_gn_tok", st, (k_mva_gn_reg<TI, TO><<<dim3(G, B * F), GN_THREADS, 0, st>>>(
+        LGM_LAUNCH("k_mva_gn_reg", st, (k_mva_gn_reg<TI, TO><<<dim3(G, B * F), GN_THREADS, 0, st>>>(
                                            F, C, HW, G, eps, (const TI *)x, gamma, beta, (TO *)tok, mean, rstd)));
         return LGM_OK;
     }
     const size_t lds = ((size_t)(C / G) * HW + 2 * (C / G)) * sizeof(float);
     if (lds <= GN_LDS_MAX) {  // one launch: the group's slab in LDS
-        static bool attr_set = false;  // (the kernel's dynamic LDS limit raised once per instantiation)
-        if (!attr_set) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mva_gn_tok<TI, TO>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)GN_LDS_MAX) != hipSuccess) {
-                set_error("hipFuncSetAttribute(k_mva_gn_tok) failed");
-                return LGM_E_HIP;
-            }
-            attr_set = true;
+        // the kernel's dynamic LDS limit is raised on every launch of this path: the attribute belongs to the current
+        // device, and a process-wide "already set" flag would skip it on a second device (and race between threads);
+        // the call is a host-side table update, no device work (include/lgm_attn.h, threading note)
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mva_gn_tok<TI, TO>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)GN_LDS_MAX) != hipSuccess) {
+            set_error("hipFuncSetAttribute(k_mva_gn_tok) failed");
+            return LGM_E_HIP;
         }
         LGM_LAUNCH("k_mva_gn_tok", st, (k_mva_gn_tok<TI, TO><<<dim3(G, B * F), GN_THREADS, lds, st>>>(
                                            F, C, HW, G, eps, (const TI *)x, gamma, beta, (TO *)tok, mean, rstd)));
@@ -1015,9 +1026,9 @@ extern "C" int lgm_mva_norm_tokens_backward(int dtype_x, int dtype_tok, int B, i
                                             const lgm_diag *diag) {
     lgm::clear_error();
     lgm::DiagScope ds(diag);
-    if (B < 0 || F <= 0 || C <= 0 || HW < 0 || groups <= 0 || C % groups || C / groups > 256) {
+    if (B < 0 || F <= 0 || C <= 0 || HW < 0 || groups <= 0 || C % groups || C / groups > lgm::GN_NMAX) {
         lgm::set_error("lgm_mva_norm_tokens_backward: bad shape B=%d F=%d C=%d HW=%d groups=%d (channels per group "
-                       "<= 256)", B, F, C, HW, groups);
+                       "<= %d)", B, F, C, HW, groups, lgm::GN_NMAX);
         return LGM_E_INVALID;
     }
     if (B == 0 || HW == 0) return LGM_OK;

@@ -324,6 +324,15 @@ int lgm_render_needle_flags(long long n, const float *abc, unsigned char *flags_
     return LGM_OK;
 }
 
+int lgm_render_det_flush_limit_log2(int views, int tiles, int scene_record) {
+    lgm::clear_error();
+    if (views <= 0 || tiles <= 0) {
+        lgm::set_error("lgm_render_det_flush_limit_log2: views and tiles must be positive");
+        return LGM_E_INVALID;
+    }
+    return lgm::det_flush_limit_log2(views, tiles, scene_record != 0);
+}
+
 int lgm_render_backward(int B, int V, int N, int H, int W, const float *gaussians, const float *cam_view,
                         const float *cam_view_proj, const float *bg, float tanfovx, float tanfovy,
                         float scale_modifier, const float *d_image, const float *d_depth, const float *d_alpha,

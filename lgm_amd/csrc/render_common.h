@@ -30,6 +30,17 @@ __host__ __device__ inline size_t acc_elems(size_t B, size_t V, size_t N) { retu
 // stored record (rec_needle) identically by the binning, the backward's flush and the preprocess backward (via a
 // flag in bit 31 of the record's rect).
 __host__ __device__ inline size_t acc_side_offset(size_t B, size_t V, size_t N) { return (acc_elems(B, V, N) + 1) & ~(size_t)1; }
+// Deterministic mode's per-flush overflow bound (k_render_bwd): in that mode an accumulator takes at most one flush
+// per tile list its Gaussian appears in -- one work item per tile, an entry once per list. A per-view record (mean2D,
+// conic, depth) sees the T tiles of its view; a per-scene record (opacity, colour: acc_index q = 5..8) the V * T
+// tiles of all views of its scene. With every flush |a| <= 2^62 / 2^ceil(log2 flushes), no sum of them reaches 2^62,
+// whatever their signs, so int64 cannot wrap. (The design value of a flush is <= ~2^51: DET_BITS below.)
+__host__ __device__ inline int det_flush_limit_log2(int V, int T, bool scene_record) {
+    const long long f = scene_record ? (long long)V * T : (long long)T;
+    int c = 0;
+    while ((1ll << c) < f) c++;  // ceil(log2 f)
+    return 62 - c;
+}
 constexpr int LDS_HIST_MAX = 8192;                   // tiles per view for the LDS-histogram binning path
 constexpr float LOG2E = 1.4426950408889634f;
 

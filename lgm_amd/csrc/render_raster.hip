@@ -804,8 +804,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     float Erem = DK - Dup;  // Dfin - K - D_i, kept directly (one subtraction less per entry)
     const float ddelx_dx = 0.5f * d.W, ddely_dy = 0.5f * d.H;
     const int det_s = DET ? det_seed_shift(det_max) : 0;
-    const float det_lim = ldexpf(1.f, d.det_lim_log2 ? d.det_lim_log2  // (2^62 / 2^ceil(log2 T))
-                                                     : 62 - (d.T > 1 ? 32 - __clz(d.T - 1) : 0));
+    // per-flush bounds of the per-view and the per-scene records (render_common.h det_flush_limit_log2)
+    const float det_lim_v = ldexpf(1.f, d.det_lim_log2 ? d.det_lim_log2 : det_flush_limit_log2(d.V, d.T, false));
+    const float det_lim_s = ldexpf(1.f, d.det_lim_log2 ? d.det_lim_log2 : det_flush_limit_log2(d.V, d.T, true));
     const size_t gbase = (size_t)bv * d.N;
     // MFMA operands: A (features) lane (ql, qk) holds feature ql of wave pixels 32 t + 8 qk + j, j = 0..7
     const int ql = lane & 15, qk = lane >> 4;
@@ -1143,12 +1144,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
                 if (a != 0.f) {
                     if (DET) {  // integer adds commute: order-independent sums (a is already in fixed-point units)
-                        // (an accumulator takes at most one flush per tile of its view -- one work item per tile
-                        // in this mode, an entry once per tile list -- so |a| <= det_lim = 2^62 / 2^ceil(log2 T)
-                        // keeps every sum below 2^62 whatever the flushes' signs; the design value is |a| <= ~2^51
-                        // per flush. A flush beyond the bound is counted and k_preproc_bwd then poisons the call's
-                        // gradients with NaN instead of returning possibly wrapped sums)
-                        if (!(fabsf(a) <= det_lim)) atomicAdd(det_sat, 1u);
+                        // (a per-view record takes at most T flushes, a per-scene one (q = 5..8) V * T: with |a|
+                        // below the record's bound no sum reaches 2^62 whatever the flushes' signs; the design value
+                        // is |a| <= ~2^51 per flush. A flush beyond the bound is counted and k_preproc_bwd then
+                        // poisons the call's gradients with NaN instead of returning possibly wrapped sums)
+                        if (!(fabsf(a) <= (q >= 5 && q < 9 ? det_lim_s : det_lim_v))) atomicAdd(det_sat, 1u);
                         atomicAdd(reinterpret_cast<unsigned long long *>(accum) + ai,
                                   (unsigned long long)__float2ll_rn(fminf(fmaxf(a, -9.0e18f), 9.0e18f)));
                     } else {

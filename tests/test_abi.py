@@ -63,3 +63,33 @@ def test_no_process_wide_switches():
             if "void *stream" in args and name not in ("lgm_render_tile_lists", "lgm_render_pixel_state",
                                                               "lgm_render_records", "lgm_render_needle_flags"):
                 assert args.rstrip().endswith("const lgm_diag *diag"), name
+
+
+def test_deterministic_flush_bound():
+    """LGM_RENDER_DETERMINISTIC's per-flush bound (render_common.h det_flush_limit_log2): per-view records take one
+    flush per tile of their view, per-scene records (opacity, colour) one per tile of every view of the scene, so
+    F flushes of at most 2^bound each stay below 2^62 and no int64 sum can wrap."""
+    L = _native.lib()
+    assert L.lgm_render_det_flush_limit_log2(6, 256, 0) == 54  # cfg3: 256 tiles per view
+    assert L.lgm_render_det_flush_limit_log2(6, 256, 1) == 51  # 1,536 flushes per scene record
+    assert L.lgm_render_det_flush_limit_log2(26, 1024, 1) == 47  # cfg5: 26 views of 512^2
+    assert L.lgm_render_det_flush_limit_log2(1, 1, 1) == 62
+    for V in (1, 2, 3, 6, 20, 26, 34):
+        for T in (1, 4, 255, 256, 257, 1024, 4096):
+            for scene in (0, 1):
+                F = V * T if scene else T
+                b = L.lgm_render_det_flush_limit_log2(V, T, scene)
+                assert F * 2 ** b <= 2 ** 62 < 2 * F * 2 ** b, (V, T, scene, b)
+    assert L.lgm_render_det_flush_limit_log2(0, 16, 0) < 0
+
+
+def test_no_function_local_static_state():
+    """SURVEY §8(b) / include/lgm_render.h: no mutable state in the library besides the thread-local error and
+    diagnostics scope -- no function-local statics (a per-process "attribute already set" flag would skip a second
+    device; mvattn.hip raises the dynamic-LDS limit on every launch instead)."""
+    for src in glob.glob(os.path.join(ROOT, "lgm_amd", "csrc", "*")):
+        for i, line in enumerate(open(src), 1):
+            code = re.sub(r'"[^"]*"', '""', line.split("//")[0])  # (no string literals)
+            m = re.search(r"\bstatic\s+(?!constexpr|thread_local)(.*)", code)
+            if m and not re.match(r"[^=;\[]*\(", m.group(1)):  # a static variable, not a static function
+                raise AssertionError(f"{os.path.basename(src)}:{i}: {line.strip()}")

@@ -158,10 +158,18 @@ def test_module_bf16_autocast(cuda, path):
 
 
 MVA_CASES = [  # C, heads, frames, H, W, batch -- LGM levels (D = 32 / 64) and ragged ones (Cg = 3: scalar stores)
-    # the LGM-shaped cases run the register-slab GroupNorm and the vector-access layout kernels; (96, ..., 7, 5)
-    # their scalar forms (HW % 4 != 0, Cg % 8 != 0); 48 x 48 at Cg = 16 the LDS-slab GroupNorm (> 1,024 items)
+    # the LGM-shaped cases run the register-slab GroupNorm (k_mva_gn_reg) and the vector-access layout kernels;
+    # (96, ..., 7, 5) their scalar forms (HW % 4 != 0, Cg % 8 != 0) and the LDS-slab GroupNorm's scalar branches;
+    # 46 x 46 at Cg = 16 the LDS-slab GroupNorm's vector path (1,058 items > 1,024; slab 135,552 B <= 144 KB);
+    # 48 x 48 at Cg = 16 the chunked fallback (slab 147,584 B > 144 KB: k_mva_stats + k_mva_norm); C = 512 in one
+    # group (Cg = 512: no register slab) the LDS slab and k_mva_gn_coef's channel loop (more channels than threads)
     (512, 16, 6, 16, 16, 1), (1024, 16, 6, 10, 10, 1), (256, 8, 4, 8, 8, 2), (96, 3, 2, 7, 5, 1),
-    (512, 16, 1, 48, 48, 1)]
+    (512, 16, 1, 46, 46, 1), (512, 16, 1, 48, 48, 1), (512, 16, 2, 4, 4, 1, 1)]
+# the GroupNorm -> tokens kernel each case must launch (KernelProfiler names, mvattn.hip launch_norm)
+MVA_GN_KERNEL = {(512, 16, 6, 16, 16, 1): "k_mva_gn_reg", (1024, 16, 6, 10, 10, 1): "k_mva_gn_reg",
+                 (256, 8, 4, 8, 8, 2): "k_mva_gn_reg", (96, 3, 2, 7, 5, 1): "k_mva_gn_tok",
+                 (512, 16, 1, 46, 46, 1): "k_mva_gn_tok", (512, 16, 1, 48, 48, 1): "k_mva_stats",
+                 (512, 16, 2, 4, 4, 1, 1): "k_mva_gn_tok"}
 
 
 @pytest.mark.gpu
@@ -173,27 +181,38 @@ def test_mvattention_fused_layout_matches_torch_ops(cuda, case, mode):
     (fused=False): forward, dL/dx and the GroupNorm / Linear parameter gradients. fp32: the only difference is the
     order of the GroupNorm sums (1e-5, forward and gradients); bf16: tokens may round to neighbouring bf16 values
     (1e-2; gradients 1e-1). The fused backward's sums run in a fixed order: two runs are bitwise equal."""
+    from lgm_amd import _native
     from lgm_amd.attention import MVAttention
-    C, heads, frames, H, W, B = case
+    C, heads, frames, H, W, B = case[:6]
+    groups = case[6] if len(case) > 6 else 32
     torch.manual_seed(11)
-    m = MVAttention(C, heads, num_frames=frames, skip_scale=0.5 ** 0.5).to(cuda)
+    m = MVAttention(C, heads, num_frames=frames, skip_scale=0.5 ** 0.5, groups=groups).to(cuda)
     with torch.no_grad():
         m.norm.weight.uniform_(0.5, 1.5)
         m.norm.bias.uniform_(-0.2, 0.2)
     x0 = torch.randn(B * frames, C, H, W, device=cuda) * 2 + 0.3
     gy = torch.randn(B * frames, C, H, W, device=cuda)
     outs = []
+    prof = _native.KernelProfiler()
     for fused in (True, True, False):
         m.fused = fused
         m.zero_grad()
         x = x0.clone().requires_grad_(True)
-        if mode == "f32":
-            y = m(x)
-        else:
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+        with prof:
+            if mode == "f32":
                 y = m(x)
-        y.float().backward(gy)
+            else:
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    y = m(x)
+            y.float().backward(gy)
+        if fused:
+            ran = prof.summary()
+            prof.reset()
+            gn = {k for k in ran if k in ("k_mva_gn_reg", "k_mva_gn_tok", "k_mva_stats")}
+            assert gn == {MVA_GN_KERNEL[case]}, (case, sorted(ran))
+            assert "k_mva_gn_coef" in ran and "k_mva_out" in ran, sorted(ran)
         outs.append((y.dtype, y.detach().float(), x.grad.float(), {k: p.grad.float() for k, p in m.named_parameters()}))
+    prof.close()
     tol, gtol = (1e-5, 1e-5) if mode == "f32" else (1e-2, 1e-1)
     (tf, yf, dxf, gf), (_, yf2, dxf2, gf2), (tt, yt, dxt, gt) = outs
     assert tf == tt
@@ -215,7 +234,27 @@ SHAPES = [  # B, L, H, D -- LGM levels (4 views x 8^2 / 16^2 / 32^2 tokens, D = 
     # D = 64 with two query sub-tiles per wave (ceil(L/128) * B * H >= 512): LGM's default training level
     # (B = 8 is sharded; 4 x 1024 crosses the threshold) and the 'big' 2400-token level at B = 2
     (4, 1024, 16, 64), (2, 2400, 16, 64),
+    # D = 32 with FOUR query sub-tiles per forward wave (ceil(L/256) * B * H >= 1,536 workgroups: LGM training's
+    # B = 8 x L 4096 level) and a partial last tile: 17 x 96 = 1,632 workgroups
+    (6, 4100, 16, 32),
 ]
+
+
+def _sdpa_errors(qkv, scale, d_o, o_t, dqkv_t, floor):
+    """The same 16-bit inputs through torch's own attention (F.scaled_dot_product_attention, whichever ROCm backend
+    torch picks) against the same fp64 truth: an independent measure of what the format allows on these inputs, so
+    the 16-bit bars are pinned to a baseline rather than to this kernel."""
+    import torch.nn.functional as F
+    x = qkv.clone().requires_grad_(True)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    o = F.scaled_dot_product_attention(q, k, v, scale=scale).transpose(1, 2)
+    o.backward(d_o)
+    torch.cuda.synchronize()
+    out = {"o": rel_l2(o.detach().double().cpu().numpy(), o_t.cpu().numpy())}
+    for i, name in enumerate("qkv"):
+        a, b = x.grad[:, :, i].double(), dqkv_t[:, :, i]
+        out["d" + name] = float((a - b).norm()) / max(float(b.norm()), floor)
+    return out
 
 
 @pytest.mark.gpu
@@ -237,14 +276,20 @@ def test_packed_attention_vs_fp64(cuda, shape, dtype, tol):
     o_t, dqkv_t = _packed_truth(qkv, scale, d_o)
     assert o.dtype == dtype and x.grad.dtype == dtype
     assert torch.isfinite(o).all() and torch.isfinite(x.grad).all()
-    assert rel_l2(o.double().cpu().numpy(), o_t.cpu().numpy()) < tol
     # per-slice relative L2, normalised by at least 1% of the whole dqkv norm: with L = 1 the softmax is constant
     # and the true dq is exactly 0 (only rounding noise of dP - delta remains)
     floor = 1e-2 * float(dqkv_t.norm())
+    errs = {"o": rel_l2(o.double().cpu().numpy(), o_t.cpu().numpy())}
     for i, name in enumerate("qkv"):
         a, b = x.grad[:, :, i].double(), dqkv_t[:, :, i]
-        err = float((a - b).norm()) / max(float(b.norm()), floor)
-        assert err < tol, (name, err)
+        errs["d" + name] = float((a - b).norm()) / max(float(b.norm()), floor)
+    sd = _sdpa_errors(qkv, scale, d_o, o_t, dqkv_t, floor) if dtype != torch.float32 else None
+    print(f"attention vs fp64 {shape} {dtype}: " + ", ".join(
+        f"{k} {v:.2e}" + (f" (sdpa {sd[k]:.2e})" if sd else "") for k, v in errs.items()))
+    for k, e in errs.items():
+        assert e < tol, (k, e)
+        if sd is not None:  # 16-bit: also no worse than torch's own attention on the same inputs (+25 %)
+            assert e <= max(1.25 * sd[k], tol / 8), (k, e, sd[k])
 
 
 @pytest.mark.gpu
@@ -254,9 +299,11 @@ def test_packed_attention_vs_fp64(cuda, shape, dtype, tol):
 def test_forward_score_jump(cuda, D, dtype, tol, jump):
     """The forward's online softmax where one key of a LATER key tile scores `jump` (log2 units) above every key of
     the first tile, for every query (or, negative, far below): the paths that raise the row reference m mid-row
-    (rare on bounded random data, so pinned here) must give the fp64 result. Gradients at 2x the bar: with a
-    near-one-hot softmax dS = P (dP - delta) is a cancellation, which amplifies the 16-bit rounding of the recomputed
-    P (f16, jump 30: dq 5.0e-3 for this kernel)."""
+    (rare on bounded random data, so pinned here) must give the fp64 result. With a near-one-hot softmax
+    dS = P (dP - delta) is a cancellation that amplifies the 16-bit rounding of the inputs and of the stored output,
+    so the gradients are held to the fixed bar OR to 1.25x the error of torch's own attention
+    (F.scaled_dot_product_attention) on the same 16-bit inputs against the same fp64 truth -- a bar set by an
+    independent implementation, not by this kernel."""
     from lgm_amd.attention import packed_attention
     B, L, H = 1, 320, 2
     scale = D ** -0.5
@@ -278,10 +325,12 @@ def test_forward_score_jump(cuda, D, dtype, tol, jump):
     assert torch.isfinite(o).all() and torch.isfinite(x.grad).all()
     assert rel_l2(o.double().cpu().numpy(), o_t.cpu().numpy()) < tol
     floor = 1e-2 * float(dqkv_t.norm())
+    sd = _sdpa_errors(qkv, scale, d_o, o_t, dqkv_t, floor)
     for i, name in enumerate("qkv"):
         a, b = x.grad[:, :, i].double(), dqkv_t[:, :, i]
         err = float((a - b).norm()) / max(float(b.norm()), floor)
-        assert err < 2 * tol, (name, err)
+        print(f"score jump {jump} D {D} {dtype} d{name}: {err:.2e} (sdpa {sd['d' + name]:.2e})")
+        assert err <= max(tol, 1.25 * sd["d" + name]), (name, err, sd["d" + name])
 
 
 @pytest.mark.gpu

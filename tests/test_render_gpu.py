@@ -140,17 +140,19 @@ def test_repeated_backward_retain_graph(cuda):
     assert rel_l2(second.cpu().numpy(), first.cpu().numpy()) < 1e-5
 
 
-def test_deterministic_saturation_poisons_and_resets(cuda):
-    """LGM_RENDER_DETERMINISTIC's overflow guard (render_raster.hip k_render_bwd flush): a flush above the per-flush
-    bound (2^62 / 2^ceil(log2 tiles): no sum of one flush per tile can wrap int64) is counted and k_preproc_bwd
-    poisons the call's gradients with NaN. The lgm_diag test hook lowers the bound to 2^1 to force that path; a
-    retain_graph repeat of the same forward without the hook (LGM_RENDER_BACKWARD_AGAIN) must not inherit the
-    count (k_det_seed_max clears it) and equals a clean backward bitwise."""
+@pytest.mark.parametrize("V", [2, 6])
+def test_deterministic_saturation_poisons_and_resets(cuda, V):
+    """LGM_RENDER_DETERMINISTIC's overflow guard (render_raster.hip k_render_bwd flush): a flush above its record's
+    bound (2^62 / 2^ceil(log2 F), F = T flushes for a per-view record, V * T for a per-scene one:
+    lgm_render_det_flush_limit_log2, tests/test_abi.py) is counted and k_preproc_bwd poisons the call's gradients
+    with NaN. The lgm_diag test hook lowers the bound to 2^1 to force that path; a retain_graph repeat of the same
+    forward without the hook (LGM_RENDER_BACKWARD_AGAIN) must not inherit the count (k_det_seed_max clears it), stays
+    below the derived multi-view bounds (finite) and equals a clean backward bitwise."""
     from lgm_amd import _native
-    g, cv, cvp = scene(N=3000, V=2, seed=5)
+    g, cv, cvp = scene(N=3000, V=V, seed=5)
     gd = g.to(cuda).requires_grad_(True)
     args = (cv.to(cuda), cvp.to(cuda), torch.ones(3, device=cuda), TAN, TAN, 64, 64)
-    w = torch.randn((1, 2, 3, 64, 64), generator=torch.Generator().manual_seed(3)).to(cuda)
+    w = torch.randn((1, V, 3, 64, 64), generator=torch.Generator().manual_seed(3)).to(cuda)
     img, _, alp = rasterize(gd, *args, deterministic=True)
     loss = (img * w).sum() + alp.sum()
     with _native.diagnostics(det_limit_log2=1):

@@ -85,7 +85,7 @@ def limiter_from_counters(rec, achieved_counter_gbs, avg_s=None):
 
 def pmc_record(kernel):
     """HBM bytes per launch of `kernel` and its limiter counters from the committed PMC profile of this workload
-    (rocprofv3 passes, gfx950-corrected: scripts/gpu_pmc.sh -> scripts/pmc_summary.py --json), or nulls."""
+    (rocprofv3 passes, gfx950-corrected: scripts/gpu_run.sh prof -> scripts/pmc_summary.py --json), or nulls."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         d = json.load(open(path))

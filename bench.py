@@ -337,7 +337,7 @@ def mva_level_bench(dev, steps: int = 10):
             step()
         torch.cuda.synchronize()
     res["kernels"] = {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in prof.summary().items()
-                      if k.startswith("k_mva")}
+                      if k.startswith("k_mva") or k.startswith("k_wgrad")}
     prof.close()
     return res
 

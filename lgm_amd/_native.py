@@ -64,6 +64,9 @@ SIGNATURES = {
     "lgm_gaussian_head_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "lgm_gaussian_head_backward": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                             _vp, _vp, _c_size, _vp, _vp]),
+    "lgm_linear_wgrad_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "lgm_linear_wgrad": (_c_int, [_c_int, _c_int, _c_int, _c_int, _vp, _c_ll, _vp, _c_ll, _vp, _vp, _vp, _c_size,
+                                  _vp, _vp]),
     "lgm_profiler_create": (_vp, []),
     "lgm_profiler_summary": (_c_int, [_vp, ctypes.c_char_p, _c_size]),
     "lgm_profiler_reset": (_c_int, [_vp]),

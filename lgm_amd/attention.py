@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 
 from . import _native as nat
+from .linear import linear as _linear16
 
 _DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
@@ -117,14 +118,20 @@ class Attention(nn.Module):
         self.attn_drop = nn.Dropout(attn_drop)
         self.proj = nn.Linear(dim, dim, bias=proj_bias)
         self.proj_drop = nn.Dropout(proj_drop)
+        self.native_wgrad = True  # (a plain attribute: not in the state_dict)
+
+    def _lin(self, lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+        # 16-bit GPU Linears take their weight gradient from the HIP split-K kernel (lgm_amd/linear.py);
+        # native_wgrad = False: torch's autograd through nn.Linear, as upstream
+        return _linear16(x, lin) if self.native_wgrad else lin(x)
 
     def _attend(self, x: torch.Tensor) -> torch.Tensor:
         if self.training and self.attn_drop.p > 0:
             raise NotImplementedError("attention-probability dropout is not implemented (LGM uses attn_drop=0)")
         B, N, C = x.shape
-        qkv = self.qkv(x).reshape(B, N, 3, self.num_heads, C // self.num_heads)
+        qkv = self._lin(self.qkv, x).reshape(B, N, 3, self.num_heads, C // self.num_heads)
         y = packed_attention(qkv, self.scale).reshape(B, N, C)
-        return self.proj_drop(self.proj(y))
+        return self.proj_drop(self._lin(self.proj, y))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self._attend(x)

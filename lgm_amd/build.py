@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/common.hip", "csrc/render_bin.hip", "csrc/render_raster.hip", "csrc/render_api.hip",
-           "csrc/attention.hip", "csrc/head.hip", "csrc/mvattn.hip"]
+           "csrc/attention.hip", "csrc/head.hip", "csrc/mvattn.hip", "csrc/wgrad.hip"]
 # per-source extra flags. attention.hip: no NaN semantics -- its max / exp chains then skip the quieting
 # canonicalisations clang inserts before every fmaxf of an MFMA result (the render kernels keep IEEE NaN handling:
 # degenerate-Gaussian tests such as !(det > 0) rely on it)

@@ -515,6 +515,12 @@ def run(args):
     from lgm_amd.gs import count_pairs
     from lgm_amd.synthetic import synthetic_gaussians, synthetic_upstream_grads
 
+    if args.only_attn:  # the attention-side lines alone (A/B runs of the attention / MVAttention kernels)
+        if rank == 0:
+            print(json.dumps({"attention": attention_bench(dev), "mva_level": mva_level_bench(dev),
+                              "cfg4": cfg4_bench(dev, max(10, args.steps // 5))}), flush=True)
+        D.finalize(info)
+        return
     renderer = GaussianRenderer(Options(output_size=RES))
     tan = float(renderer.tan_half_fov)
     cv, cvp, cp = orbit_cameras(VIEWS)
@@ -720,6 +726,8 @@ def parse(argv=None):
     ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 (LGM 'big') hot-path measurement")
     ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 (training step, render side) measurement")
     ap.add_argument("--no-det", action="store_true", help="skip the deterministic-mode timing of the pool")
+    ap.add_argument("--only-attn", action="store_true",
+                    help="only the attention, MVAttention-level and cfg4 lines (attention-side A/B runs)")
     ap.add_argument("--only-pool", action="store_true",
                     help="only the headline workload (for counter profiles: no other kernel launches of other sizes)")
     return ap.parse_args(argv)

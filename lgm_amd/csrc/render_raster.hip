@@ -85,7 +85,10 @@ struct StageT {                                   // PAD: list padding = entries
 // saturate within a chunk or two, and the prefetch costs LDS and registers); FWD_FU = 4 entries evaluated per step
 // (8 per step spilled). Backward: 64-entry chunks, double-buffered.
 constexpr int FWD_FU = 4;
-using StageFwd = StageT<1, FWD_FU>;
+#ifndef LGM_FWD_SMALL_TILES
+#define LGM_FWD_SMALL_TILES 256
+#endif
+constexpr int FWD_SMALL_TILES = LGM_FWD_SMALL_TILES;  // launches of at most this many tiles take k_render_fwd<., 8>
 constexpr int BWD_CHUNK = 64;
 // backward lists are padded to MB with the sentinel: every list position is one MFMA batch column (k_render_bwd)
 using StageBwd = StageT<2, MB, BWD_CHUNK>;
@@ -203,8 +206,12 @@ __device__ __forceinline__ void init_sentinel(Stage &S) {
 
 // k_render_fwd: grid (B*V*T), block 256, tile xcd_item(blockIdx). 7 waves per SIMD: <= 72 VGPRs (spills outside
 // the compositing loop only): 327 vs 336 us at 6, 411 at 8 (pool).
-template <bool LOSS>  // LGM_RENDER_FUSED_LOSS compiled in (its epilogue registers stay out of the plain kernel)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_render_fwd(Dims d, long long slot_stride,
+// FU: entries evaluated per step. 4 for every launch that fills the chip; launches of at most one tile per CU
+// (FWD_SMALL_TILES: a single 256^2 view, BASELINE config 2) run one wave per SIMD, where nothing hides a wave's own
+// dependency chains, and take FU = 8 at 2 waves per SIMD (more registers: twice the independent evaluations in flight).
+// The serial T / colour chain is in list order either way: the outputs are bitwise the same.
+template <bool LOSS, int FU>  // LOSS: LGM_RENDER_FUSED_LOSS compiled in (its epilogue registers stay out otherwise)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FU == FWD_FU ? 7 : 2))) void k_render_fwd(Dims d, long long slot_stride,
                                                     const int *__restrict__ tile_start,
                                                     const int *__restrict__ tile_count,
                                                     const unsigned long long *__restrict__ pairs,
@@ -219,7 +226,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                                                     int *__restrict__ nck, unsigned *__restrict__ ckctr,
                                                     int ck_region, float4 *__restrict__ zero_base,
                                                     long long zero_n16) {
-    __shared__ StageFwd S;
+    __shared__ StageT<1, FU> S;
     __shared__ int s_ck[2];
     const int tile = xcd_item(blockIdx.x, d.BV * d.T);
     const int bv = tile / d.T, t = tile - bv * d.T, b = bv / d.V;
@@ -240,7 +247,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     // Tr < 0 marks a saturated pixel (|Tr| its final transmittance): outside pixels start saturated
     float Tr = inside ? 1.0f : -1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     int last = 0;
-    constexpr int FU = FWD_FU;
     unsigned c_iter = 0, c_list = 0;  // diagnostic work counters (Dims::counters)
     // Staging: chunk c's entries land by LDS DMA, synchronously; the sorted ids run two chunks ahead in registers.
     // Each lane tests its own entry as soon as its row has landed, so one barrier publishes rows and masks together.
@@ -697,22 +703,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // 8 consecutive entry columns land on distinct banks (ds_write_b32 banks are (a / 4) mod 32)
     // (the depth-gradient instantiation keeps stride 65 and one shared junk row: its larger slots would not leave
     // room for a fourth workgroup per CU otherwise)
-    constexpr int CH = BWD_CHUNK, LS = DEPTH ? CH + 1 : CH + 4;
+    constexpr int CH = BWD_CHUNK, LS = CH + 4;
     __shared__ StageBwd S;
     // per-wave moment slots (plain stores: each wave writes an entry's moments once; no LDS atomics), combined over
-    // the entry's quadrant waves at the chunk's end (then they hold the entry's gradient partials, in wave 0's slot)
-    // moment rows: 0..5 geometric (w columns), then dL/dpixel-hi and dL/dpixel-lo sums of the NC colour [+ depth]
-    // channels (u columns). The MFMA results a lane does not keep go to a junk area after the rows (JB), each lane
-    // class of a store to its own 8-bank range there (mrow below), so the stores need no exec-masked branches and
-    // put no two lanes of a 32-lane group on one bank while the batch's columns are consecutive
-    constexpr int NC = DEPTH ? 4 : 3, NROW = 6 + 2 * NC;
-    constexpr int JB = DEPTH ? LS * NROW : (LS * NROW + 31) & ~31;
-    constexpr int SLOT = DEPTH ? (LS * (NROW + 1) + 3) & ~3 : JB + 32 + CH + 4;  // 16-B aligned slots
-    constexpr int ZSLOT = (LS * NROW + 3) & ~3;  // the part zeroed per chunk (the junk area is never read)
+    // the entry's quadrant waves after the entries loop. Rows 0..5 geometric (w columns), then one row per colour
+    // [+ depth] channel (u columns): the A operand holds each channel's dL/dpixel hi and lo bf16 parts in adjacent
+    // rows (6 + 2c, 7 + 2c: one lane's accumulator pair), so a lane adds the pair before storing and the slot keeps
+    // NC colour rows, not 2 NC. The MFMA results a lane does not keep go to a junk word after the rows (JB + lane +
+    // the batch column; never read), so the stores need no exec-masked branches.
+    constexpr int NC = DEPTH ? 4 : 3, NROW = 6 + NC, NROWA = 6 + 2 * NC;
+    constexpr int JB = (LS * NROW + 3) & ~3;
+    constexpr int SLOT = JB + 64 + CH + 4;        // junk words JB + lane + column; 16-B aligned slots
+    constexpr int ZSLOT = JB;                     // the part zeroed per chunk (the junk words are never read)
     __shared__ __attribute__((aligned(16))) float sAccW[4][SLOT];
     __shared__ __attribute__((aligned(16))) float sWU[4][16 * WU_LD];  // read as float4: keep 16-B aligned
-    static_assert((NV + 3) * LS <= 16 * WU_LD, "the partial rows fit wave 0's WU image");
-    __shared__ int s_ndl;  // the chunk holds a needle-like record (its conic partials go to the fp64 side block)
+    // the chunk's gradient partials (rows q * LS + j; a needle's conic partials in rows NV .. NV + 2 for the fp64
+    // flush) and its Gaussian ids, written by the conversion and read by the flush. Their own buffer (not a dead WU
+    // image) lets a wave start the next chunk's quadrant tests and entries right after its share of the flush, while
+    // other waves still flush: one barrier less per chunk
+    __shared__ __attribute__((aligned(16))) float sO[(NV + 3) * LS];
+    __shared__ unsigned sId[CH];
+    __shared__ int s_ndl[2];  // chunk parity: the chunk holds a needle-like record (conic partials to the fp64 block)
 
     // ---- work item: (tile, chunk c, checkpoint slot)
     const int M = d.BV * d.T, Mp = round8(M);  // head items, then the checkpoint items (none in deterministic mode)
@@ -811,24 +822,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // MFMA operands: A (features) lane (ql, qk) holds feature ql of wave pixels 32 t + 8 qk + j, j = 0..7
     const int ql = lane & 15, qk = lane >> 4;
     const float cxT = (float)tx0 + 7.5f, cyT = (float)ty0 + 7.5f;
-    // the slot row offset of this lane's result r (row 4 qk + r of column ql), -1 where that result is unused:
-    // w columns keep the geometric moments (rows 0..5), u columns the colour / depth sums (rows 6..8 [9])
-    // Banks: with LS = 4 (mod 32) the four lane classes of a 32-lane store group -- (qk, w or u column) for the
-    // group's two qk -- sit at rr LS + 8 m (mod 32), m = 0..3: a live row 4 qk + rr at m = 2 (qk & 1), the dead
-    // classes on the free m, so the group's 32 lanes cover the 32 banks once (8 consecutive columns per class).
+    // the slot offset of this lane's r-th stored value: w columns (ql < MB) keep D rows 4 qk + r <= 5 (the geometric
+    // moments); u columns keep the sums of the accumulator pairs (r = 0: D rows 4 qk, 4 qk + 1; r = 1: 4 qk + 2, + 3)
+    // that are a colour channel's hi / lo rows 6 + 2c, 7 + 2c -> slot row 6 + c. Everything else: the junk word.
     int mrow[4];
-    static_assert(DEPTH || LS % 32 == 4, "moment-slot bank layout");
 #pragma unroll
     for (int rr = 0; rr < 4; rr++) {
-        auto is_live = [&](int qq, bool ucol) {
-            const int row = 4 * qq + rr;
-            return ucol ? (row >= 6 && row < NROW) : row <= 5;
-        };
-        const bool ucol = ql >= MB;
-        const int row = 4 * qk + rr;
-        const bool live = is_live(qk, ucol);
-        const int m = 2 * (qk & 1) + (live ? 0 : (is_live(qk, !ucol) || ucol ? 1 : 0));
-        mrow[rr] = live ? row * LS : DEPTH ? JB : JB + ((rr * LS + 8 * m) & 31);
+        int row = -1;
+        if (ql < MB) {
+            if (4 * qk + rr <= 5) row = 4 * qk + rr;
+        } else if (rr < 2) {
+            const int a = 4 * qk + 2 * rr;  // the pair's first D row
+            if (a >= 6 && a < NROWA) row = 6 + (a - 6) / 2;
+        }
+        mrow[rr] = row >= 0 ? row * LS : JB + lane;
     }
     float *myAcc = sAccW[w];
     float *myWU = sWU[w];
@@ -845,8 +852,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     bf16x8 Ah[2];
     {
         const float fx0 = (float)((w & 1) << 3) - 7.5f, fy0 = (float)((w >> 1) << 3) - 7.5f;
-        const bool isdp = ql >= 6 && ql < NROW, islo = ql >= 6 + NC;
-        const int qd = isdp ? (islo ? ql - 6 - NC : ql - 6) : 0;  // the dL/dpixel channel of rows 6..NROW-1
+        const bool isdp = ql >= 6 && ql < NROWA, islo = isdp && ((ql - 6) & 1);
+        const int qd = isdp ? (ql - 6) >> 1 : 0;  // the dL/dpixel channel of rows 6..NROWA-1 (hi, lo per channel)
 #pragma unroll
         for (int t2 = 0; t2 < 2; t2++) {
             const float fy = fy0 + (float)(4 * t2 + qk);
@@ -913,36 +920,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             a2[t2] = cacc;
         }
         const f32x4 acc = a2[0] + a2[1];
-        // D[row = 4 qk + r][col = ql]: moments 0..5 in the w columns, rows 6..9 in the u columns; each lane stores its
-        // (at most 4) live results into this wave's slots at a per-lane row offset fixed for the kernel (mrow)
-#pragma unroll
-        for (int rr = 0; rr < 4; rr++) myAcc[mrow[rr] + col] = acc[rr];  // (sentinel columns: row CH, all zero)
+        // D[row = 4 qk + r][col = ql]: moments 0..5 in the w columns; in the u columns each colour channel's hi and lo
+        // rows are one lane's pair (r, r + 1), added here (the same sum the conversion formed before: bitwise equal);
+        // each lane stores its values at per-lane offsets fixed for the kernel (mrow; dead ones to its junk word)
+        const bool ucol = ql >= MB;
+        const float v0 = ucol ? acc[0] + acc[1] : acc[0], v1 = ucol ? acc[2] + acc[3] : acc[1];
+        myAcc[mrow[0] + col] = v0;  // (sentinel columns: row CH, all zero)
+        myAcc[mrow[1] + col] = v1;
+        myAcc[mrow[2] + col] = acc[2];
+        myAcc[mrow[3] + col] = acc[3];
     };
 
     // Staging pipeline (front to back over [s0, s1)): chunk b0 + CH streams into the other buffer by LDS DMA
     // during chunk b0's compositing and is complete (vm_wait_all) before chunk b0's gradient atomics are issued,
     // so no staging load queues behind them; the sorted ids run one chunk further ahead in a register.
+    // Two barriers per chunk: P (after the entries loop: every wave's moments are in its slot) and F (before the
+    // flush: the partials are in sO, and the stager's next chunk has landed). The chunk-top barrier of rounds 1-5 is
+    // gone: a wave goes from its share of chunk c's flush straight into chunk c + 1's quadrant tests and entries
+    // while the others still flush. That is safe because nothing the flush reads is written before the next P:
+    // the partials and ids live in sO / sId (rewritten only by the next conversion, after P), the needle flag has one
+    // word per chunk parity, and the next chunk's DMA overwrites the buffer of chunk c - 1, whose last reader (the
+    // conversion of c - 1) finished before F of c - 1. Each wave zeroes its own moment slot at the top of a chunk,
+    // after the conversion that read it (before F).
     vm_wait_all();
+    __syncthreads();  // the first chunk's rows and the sentinel rows
     int cur = 0;
 #ifdef LGM_BWD_STAMPS
     SEC_T(ts_loop);
     SEC_ADD(sec[0], ts_item, ts_loop);  // prologue: pixel state, seeds, MFMA operands, first staging
 #endif
-    for (int b0 = s0; b0 < s1; b0 += CH, cur ^= 1) {
-#ifdef LGM_BWD_STAMPS
-        SEC_T(ts_c0);
-#endif
-        __syncthreads();
+    for (int b0 = s0, ci = 0; b0 < s1; b0 += CH, cur ^= 1, ci++) {
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c0b);
-        SEC_ADD(sec[1], ts_c0, ts_c0b);
 #endif
         auto &B = S.buf[cur];
         const int k = b0 + tid;
         // one row per lane: every wave tests all CH entries against its OWN quadrant (one ellipse test per lane
         // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
         if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
-        if (!DET && tid == 0) s_ndl = 0;  // (published by the barrier after the entries loop)
+        if (!DET && tid == 0) s_ndl[ci & 1] = 0;  // (published by P; the flush of chunk ci - 2 read it before P of ci - 1)
         {  // every wave zeroes its own slot (an entry it skips, or never lists, adds nothing): wave-private, so the
            // entries loop follows the quadrant tests without a barrier (with the conversion over three waves below:
            // pool k_render_bwd 642 -> 635 us, bitwise equal, profiles/r04/ab_bwd_conv)
@@ -969,7 +985,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         static_assert(MB == 8, "one batch = two 4-entry list words");
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c1);
-        SEC_ADD(sec[2], ts_c0b, ts_c1);  // chunk head: quadrant tests + compaction, next DMA issue
+        SEC_ADD(sec[2], ts_c0b, ts_c1);  // chunk head: quadrant tests + compaction, next DMA issue ([1]: unused)
 #endif
         const int lastrel = last - b0;  // this pixel's last contributor, relative to the chunk
         uint2 lraw[2];  // the next step's list words, read one step ahead
@@ -1050,10 +1066,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #endif
         __syncthreads();
         // moments -> gradient partials, an entry's three groups on three waves at once (thread 64 g + j, entry j):
-        // g = 0 mean2D + opacity (moment rows 0..2), g = 1 conic (rows 0..5; a needle's go to rows NV..NV+2 for the
-        // fp64 flush), g = 2 colour [+ depth] (the hi + lo rows). The partials go to wave 0's WU image (dead until
-        // the next chunk's entries loop, which starts after that chunk's first barrier), rows q * LS + j.
-        float *o = sWU[0];
+        // g = 0 mean2D + opacity (moment rows 0..2) and the entry's Gaussian id, g = 1 conic (rows 0..5; a needle's go
+        // to rows NV..NV+2 for the fp64 flush), g = 2 colour [+ depth] (the summed hi + lo rows). The partials go to
+        // sO, rows q * LS + j.
+        float *o = sO;
         if (w < 3 && b0 + lane < s1) {  // (w: wave-uniform)
             const int j = lane;
             auto msum = [&](int row) {
@@ -1067,7 +1083,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 for (int qq = 6; qq < NV; qq++) {
                     float v = 0.f;
 #pragma unroll
-                    for (int ww = 0; ww < 4; ww++) v += sAccW[ww][qq * LS + j] + sAccW[ww][(qq + NC) * LS + j];
+                    for (int ww = 0; ww < 4; ww++) v += sAccW[ww][qq * LS + j];  // (each term: that wave's hi + lo)
                     o[qq * LS + j] = DET ? ldexpf(v, det_s) : v;
                 }
             } else {
@@ -1080,6 +1096,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 DetNorm nm;
                 if (DET) nm = det_norm(Pj.z, Pj.w, Qj.x, d.W, d.H);
                 if (w == 0) {
+                    sId[j] = reinterpret_cast<const unsigned *>(&B.R[j])[3];
                     const float Sx = fmaf(xg, q0, -q1), Sy = fmaf(yg, q0, -q2);
                     float p0 = -ddelx_dx * (cA * Sx + cB * Sy);
                     float p1 = -ddely_dy * (cC * Sy + cB * Sx);
@@ -1108,7 +1125,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                         o[(2 + qq) * LS + j] = ndl ? 0.f : pc[qq];
                         if (!DET) o[(NV + qq) * LS + j] = ndl ? pc[qq] : 0.f;
                     }
-                    if (ndl) s_ndl = 1;  // (benign race: every writer stores 1)
+                    if (ndl) s_ndl[ci & 1] = 1;  // (benign race: every writer stores 1)
                 }
             }
         }
@@ -1140,7 +1157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             const int j = f / NACC, q = f - j * NACC;
             if (q < NV && j < CH && b0 + j < s1) {
                 const float a = o[q * LS + j];
-                const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
+                const unsigned gid = sId[j];
                 const size_t ai = acc_index(q, gbase + gid, (size_t)b * d.N + gid, (size_t)d.BV * d.N);
                 if (a != 0.f) {
                     if (DET) {  // integer adds commute: order-independent sums (a is already in fixed-point units)
@@ -1157,14 +1174,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 }
             }
         }
-        if (!DET && s_ndl) {  // (workgroup-uniform) the chunk's needle conic partials, fp64
+        if (!DET && s_ndl[ci & 1]) {  // (workgroup-uniform) the chunk's needle conic partials, fp64
             int tt = tid;
             asm volatile("" : "+v"(tt));  // (recomputed here: lane indices hoisted out of the chunk loop spilled)
             for (; tt < 3 * CH; tt += 256) {  // (one pass at CH <= 85)
                 const int j = tt % CH, c3 = tt / CH;
                 const float a = o[(NV + c3) * LS + j];
                 if (a != 0.f && b0 + j < s1) {
-                    const unsigned gid = reinterpret_cast<const unsigned *>(&B.R[j])[3];
+                    const unsigned gid = sId[j];
                     // (the side block's offset recomputed here from the SGPR dims: a pointer hoisted out of the
                     // chunk loop was kept in VGPRs and spilled)
                     const size_t so = acc_side_offset(d.B, d.V, d.N) / 2;
@@ -1454,7 +1471,9 @@ __global__ __launch_bounds__(256) void k_preproc_bwd(Dims d, const float *__rest
 // ------------------------------------------------------------------------------------------------------------
 int launch_render_fwd(const Dims &d, const float *gaussians, const float *bg, float *image, float *depth,
                       float *alpha, char *ws, const Layout &L, hipStream_t st) {
-    auto fwd = (d.options & LGM_RENDER_FUSED_LOSS) ? k_render_fwd<true> : k_render_fwd<false>;
+    const bool small = d.BV * d.T <= FWD_SMALL_TILES;
+    auto fwd = (d.options & LGM_RENDER_FUSED_LOSS) ? (small ? k_render_fwd<true, 8> : k_render_fwd<true, FWD_FU>)
+                                                   : (small ? k_render_fwd<false, 8> : k_render_fwd<false, FWD_FU>);
     LGM_LAUNCH("k_render_fwd", st, (fwd<<<(unsigned)(d.BV * d.T), 256, 0, st>>>(
                                        d, L.slot ? (long long)d.N : -1LL, (const int *)(ws + L.tile_start),
                                        (const int *)(ws + L.tile_count), (const unsigned long long *)(ws + L.pairs),

@@ -353,16 +353,29 @@ def cfg2_bench(dev, steps):
     g = synthetic_gaussians(1, 50_000, seed=CFG2_SEED).to(dev)
     cv, cvp, cp = (t[None].to(dev) for t in orbit_cameras(1))
     bg = torch.ones(3, device=dev)
+    from lgm_amd import _native
     from lgm_amd import dist as D
     with torch.no_grad():
         D.warm_up(lambda: r.render(g, cv, cvp, cp, bg_color=bg), 5, torch.cuda.synchronize)
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        st.record()
         for _ in range(steps):
             r.render(g, cv, cvp, cp, bg_color=bg)
+        en.record()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        prof = _native.KernelProfiler()  # per-kernel HIP-event times (a separate, untimed pass)
+        with prof:
+            for _ in range(steps):
+                r.render(g, cv, cvp, cp, bg_color=bg)
+            torch.cuda.synchronize()
+        kern = prof.summary()
+        prof.close()
     return {"workload": "cfg2: 50k Gaussians x 1 view x 256^2, forward only", "ms_per_step": round(1e3 * el / steps, 4),
-            "Mpixels_per_s": round(steps * RES * RES / el / 1e6, 2)}
+            "Mpixels_per_s": round(steps * RES * RES / el / 1e6, 2),
+            "gpu_span_ms_per_step": round(st.elapsed_time(en) / steps, 4),  # (stream events around the loop)
+            "kernels": {k: {"avg_us": round(1e3 * v / n, 2), "launches": n} for k, (n, v) in kern.items()}}
 
 
 # LGM 'big' at BASELINE config 4 (core/options.py:93-103 with 6 input views at input_size 320, splat 160): the

@@ -11,7 +11,9 @@
 //     read (ds_read_b64_tr_b16): a 32-row stage of dy and of x is copied into LDS by LDS DMA (global_load_lds, no
 //     staging registers) as 256-B rows whose 32-B chunks are XOR-swizzled by the row (chunk c of row r at c ^ (r & 7)),
 //     which puts the 8 rows of every 32-lane half of a transposed read on distinct banks;
-//   * a 4-stage LDS ring with three stages in flight (counted vmcnt waits), one barrier per stage;
+//   * a 4-stage LDS ring with three stages in flight (counted vmcnt waits), one barrier per stage (fragments of stage
+//     j + 1 read during stage j's MFMAs, software-pipelined at 210 VGPRs, measured slower: 59.7 -> 64-65 us per
+//     launch, profiles/r06/ab_wgrad_pipe);
 //   * 4 waves per workgroup in 2 x 2, each a 64 x 64 block = 16 v_mfma_f32_16x16x32 per stage;
 //   * db on the same MFMAs: the dy fragment times a ones operand gives the column sums; each workgroup adds the
 //     stages whose index is congruent to its column tile (so the work is spread over the column tiles), and the
@@ -171,8 +173,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
         for (int u = 0; u < 4; u++)
 #pragma unroll
             for (int v = 0; v < 4; v++) acc[4 * u + v] = mfma<DT>(fa[u], fb[v], acc[4 * u + v]);
-        // column sums of dy: this tile's share of the stages (index = nt mod NT); waves (wm, 0) and (wm, 1) take
-        // the two halves of their 64 rows
         if (want_db && (st0 + j) % NT == nt) {
             dbacc[0] = mfma<DT>(fa[2 * wn], ones, dbacc[0]);
             dbacc[1] = mfma<DT>(fa[2 * wn + 1], ones, dbacc[1]);
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 }
 
 // k_wgrad_reduce: grid (ceil(tiles * 4096 / 256) + [ceil(Mp / 256)]), block 256. One thread per (tile, wave,
-// fragment, lane) float4 position: the S partials summed in split order (8 loads in flight), the 4 values scattered to
+// fragment, lane) float4 position: the S partials summed in split order (up to 16 loads in flight), the 4 values scattered to
 // dw; then (db) one thread per row: the NT * S column-sum partials in order.
 __global__ __launch_bounds__(256) void k_wgrad_reduce(int M, int N, int S, int NT, int tiles,
                                                       const f32x4 *__restrict__ part, const float *__restrict__ dbpart,
@@ -199,15 +199,15 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(int M, int N, int S, int N
     const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
     if (p < npos) {
         f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-        int s = 0;
-        for (; s + 8 <= S; s += 8) {
-            f32x4 v[8];
+        for (int s = 0; s < S; s += 16) {  // up to 16 partials in flight per thread (S <= 16: one round trip)
+            f32x4 v[16];
 #pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = part[(size_t)(s + u) * npos + p];
+            for (int u = 0; u < 16; u++)
+                v[u] = s + u < S ? part[(size_t)(s + u) * npos + p] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int u = 0; u < 8; u++) sum += v[u];
+            for (int u = 0; u < 16; u++)
+                if (s + u < S) sum += v[u];  // (split order)
         }
-        for (; s < S; s++) sum += part[(size_t)s * npos + p];
         const int lane = (int)(p & 63), f = (int)((p >> 6) % FRAGS), w = (int)((p >> 10) & 3);
         const int tile = (int)(p >> 12), mt = tile / NT, nt = tile - mt * NT;
         const int a = f >> 2, b = f & 3, g = lane >> 4, j = lane & 15;

@@ -12,8 +12,9 @@
 #   benchargs=ARGS       bench.py ARGS once (e.g. "benchargs=--steps 40 --only-pool")
 #   prof                 rocprofv3 --kernel-trace --stats of the default bench + per-grid split, then one rocprofv3
 #                        run per PMC pass of scripts/pmc_passes.txt (counters only with --kernel-trace)
-#   ab                   interleaved A/B of lgm_amd/_lib/variants/lib_*.so (render: bench kernel times + output hashes)
+#   ab[=LIBS]            interleaved A/B of lgm_amd/_lib/variants/lib_*.so (render: bench kernel times + output hashes)
 #   abattn               the same for the attention kernels (scripts/bench_attn.py)
+#   abmva[=LIBS]         bench.py --only-attn per variant library (MVAttention level, attention, cfg4)
 #   py=SCRIPT [ARGS]     python SCRIPT ARGS (a diagnostic under scripts/), output to $OUT/<script>.log
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=${OUT:-gpurun_out/run}
@@ -67,9 +68,11 @@ for step in "$@"; do
       done < scripts/pmc_passes.txt
       python scripts/pmc_summary.py "$OUT/pmc" --json "$OUT/pmc_latest.json" > "$OUT/pmc_summary.txt"; echo "pmc summary rc=$?" ;;
     ab)
-      OUTAB="$OUT/ab" bash scripts/gpu_ab.sh || exit $? ;;
+      OUTAB="$OUT/ab" AB_LIBS="$arg" bash scripts/gpu_ab.sh || exit $? ;;
     abattn)
       OUTAB="$OUT/ab" bash scripts/gpu_ab_attn.sh || exit $? ;;
+    abmva)
+      OUTAB="$OUT/ab" AB_LIBS="$arg" bash scripts/gpu_ab_mva.sh || exit $? ;;
     py)
       # shellcheck disable=SC2086
       set -- $arg; s=$1; shift

@@ -754,11 +754,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // the first chunk's ids and LDS DMA go out before the per-pixel state loads (bounded by the list length n, a
     // superset of [s0, s1): rows past s1 are staged but never listed or flushed), so their two dependent memory
     // round trips overlap the pixel loads instead of following them
-    const bool stager = tid < BWD_CHUNK;
+#ifdef LGM_BWD_W3STAGE
+    // wave 3 stages (and issues no gradient atomics); waves 0-2 convert and flush (their atomics are never waited for)
+    constexpr int SW = 3;
+#else
+    constexpr int SW = 0;
+#endif
+    const bool stager = w == SW;
     const int s0e = c * TILE_PIX;
-    unsigned id_cur = stager && s0e + tid < n ? ids[s0e + tid] : 0u;
-    if (stager && s0e + tid < n) stage_dma(S.buf[0], w, id_cur, (size_t)bv * d.N, b, d.N, gP, gQ, gauss);
-    unsigned id_next = stager && s0e + BWD_CHUNK + tid < n ? ids[s0e + BWD_CHUNK + tid] : 0u;
+    unsigned id_cur = stager && s0e + lane < n ? ids[s0e + lane] : 0u;
+    if (stager && s0e + lane < n) stage_dma(S.buf[0], 0, id_cur, (size_t)bv * d.N, b, d.N, gP, gQ, gauss);
+    unsigned id_next = stager && s0e + BWD_CHUNK + lane < n ? ids[s0e + BWD_CHUNK + lane] : 0u;
     const size_t P = (size_t)d.H * d.W;
     const size_t pid = inside ? (size_t)d.W * py + px : 0;
     const float T_final = inside ? final_T[bv * P + pid] : 0.f;
@@ -954,10 +960,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         SEC_T(ts_c0b);
 #endif
         auto &B = S.buf[cur];
-        const int k = b0 + tid;
         // one row per lane: every wave tests all CH entries against its OWN quadrant (one ellipse test per lane
         // instead of four per staging thread) and the ballot is its compaction mask (no shared mask, no barrier)
-        if (w == 0) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
+        if (stager) reinterpret_cast<unsigned *>(&B.R[lane])[3] = id_cur;  // for the gradient flush
         if (!DET && tid == 0) s_ndl[ci & 1] = 0;  // (published by P; the flush of chunk ci - 2 read it before P of ci - 1)
         {  // every wave zeroes its own slot (an entry it skips, or never lists, adds nothing): wave-private, so the
            // entries loop follows the quadrant tests without a barrier (with the conversion over three waves below:
@@ -979,9 +984,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
             constexpr int PAD = (int)(sizeof(S.list[0]) / sizeof(S.list[0][0])) - CH;
             if (lane < PAD) S.list[w][cnt + lane] = (unsigned short)CH;
         }
-        if (stager && k + CH < s1) stage_dma(S.buf[cur ^ 1], w, id_next, gbase, b, d.N, gP, gQ, gauss);
+        if (stager && b0 + lane + CH < s1) stage_dma(S.buf[cur ^ 1], 0, id_next, gbase, b, d.N, gP, gQ, gauss);
         id_cur = id_next;
-        id_next = stager && k + 2 * CH < s1 ? ids[k + 2 * CH] : 0u;
+        id_next = stager && b0 + lane + 2 * CH < s1 ? ids[b0 + lane + 2 * CH] : 0u;
         static_assert(MB == 8, "one batch = two 4-entry list words");
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c1);
@@ -1133,8 +1138,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         SEC_T(ts_c3);
         SEC_ADD(sec[4], ts_c2, ts_c3);  // barrier + moments -> partials
 #endif
+#ifdef LGM_BWD_W3STAGE
+        if (stager) vm_wait_all();  // the next chunk's rows and ids (only the stager has anything to wait for)
+#else
         // the next chunk's DMA and ids have landed before the atomics below go out (they cannot delay it)
         vm_wait_all();
+#endif
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c3a);
         SEC_ADD(sec[5], ts_c3, ts_c3a);  // DMA wait (and any earlier outstanding vector-memory op of this wave)
@@ -1146,15 +1155,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #endif
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
-        constexpr int FT = 256;  // flushing threads
+#ifdef LGM_BWD_W3STAGE
+        constexpr int FT = 192, FQ = NV;  // waves 0-2 flush, CH * NV items exactly (3 passes at NV = 9)
+        if (w < 3) {
+#else
+        constexpr int FT = 256, FQ = NACC;  // flushing threads; items per entry in the lane mapping
+        {
+#endif
         int ft = tid;
         // the lane's (entry, partial) indices recomputed per chunk: hoisted out of the chunk loop, their 64-bit
         // per-scene accumulator offsets were spilled, and each reload's vmcnt(0) waited for this flush's earlier atomics
         asm volatile("" : "+v"(ft));
 #pragma unroll
-        for (int it = 0; it < (CH * NACC + FT - 1) / FT; it++) {
+        for (int it = 0; it < (CH * FQ + FT - 1) / FT; it++) {
             const int f = it * FT + ft;
-            const int j = f / NACC, q = f - j * NACC;
+            const int j = f / FQ, q = f - j * FQ;
             if (q < NV && j < CH && b0 + j < s1) {
                 const float a = o[q * LS + j];
                 const unsigned gid = sId[j];
@@ -1177,7 +1192,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         if (!DET && s_ndl[ci & 1]) {  // (workgroup-uniform) the chunk's needle conic partials, fp64
             int tt = tid;
             asm volatile("" : "+v"(tt));  // (recomputed here: lane indices hoisted out of the chunk loop spilled)
-            for (; tt < 3 * CH; tt += 256) {  // (one pass at CH <= 85)
+            for (; tt < 3 * CH; tt += FT) {  // (one pass)
                 const int j = tt % CH, c3 = tt / CH;
                 const float a = o[(NV + c3) * LS + j];
                 if (a != 0.f && b0 + j < s1) {
@@ -1189,6 +1204,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
                 }
             }
         }
+        }  // (flushing waves)
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c4);
         SEC_ADD(sec[7], ts_c3b, ts_c4);  // gradient atomics (issue)

@@ -36,10 +36,14 @@ typedef __attribute__((ext_vector_type(8))) short s8v;
 
 constexpr int BM = 128, BN = 128;  // output tile (dw rows x columns) of one workgroup
 constexpr int BK = 32;             // K rows per stage (one MFMA K step)
-constexpr int RING = 4;            // LDS stages; RING - 1 in flight
+#ifndef LGM_WGRAD_RING
+#define LGM_WGRAD_RING 4
+#endif
+constexpr int RING = LGM_WGRAD_RING;  // LDS stages; RING - 1 in flight
 constexpr int THREADS = 256;
 constexpr int IMG = BK * 256;      // bytes of one operand's stage image (32 rows x 128 16-bit columns)
-constexpr int SLOTS = 512;         // workgroup slots the split targets (2 per CU: 64 KB of LDS each)
+constexpr int WPE = 2 * 4 / RING + (RING == 3 ? 1 : 0);  // workgroups (= waves per SIMD) per CU: 64 KB (ring 4) -> 2, 48 KB -> 3
+constexpr int SLOTS = 256 * WPE;   // workgroup slots the split targets
 constexpr int FRAGS = 16;          // 16 x 16 accumulator blocks per wave
 
 template <int DT> struct Op;
@@ -115,7 +119,7 @@ __device__ __forceinline__ int xcd_item(int b, int M) {
 // k_wgrad: grid (tiles * S), block 256, 64 KB of LDS. Workgroup -> (split s, tile (mt, nt)); split s covers the
 // stages [s q + min(s, r), ...) of the ceil(K / 32) stages (q, r = divmod(stages, S)).
 template <int DT>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void k_wgrad(
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(WPE))) void k_wgrad(
     int K, int M, int N, const uint16_t *__restrict__ dy, long long ld_dy, const uint16_t *__restrict__ x,
     long long ld_x, int S, int NT, f32x4 *__restrict__ part, float *__restrict__ dbpart, int Mp) {
     __shared__ __attribute__((aligned(1024))) unsigned char sA[RING][IMG];
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     // the last one, staged through registers (its loads are waited for by the compiler before the LDS stores, which
     // also drains every earlier DMA: the counted waits below stay correct)
     auto issue = [&](int j) {
-        const int k0 = (st0 + j) * BK, b = j & (RING - 1);
+        const int k0 = (st0 + j) * BK, b = j % RING;
         if (k0 + BK <= K) {
             stage<false>(dy, ld_dy, k0, K, m0, M, sA[b]);
             stage<false>(x, ld_x, k0, K, n0, N, sB[b]);
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
         else vm_wait<0>();
         __syncthreads();  // every wave's copies of stage j have landed; slot (j - 1) % RING is free
         if (j + RING - 1 < nst) issue(j + RING - 1);
-        const unsigned char *a_img = sA[j & (RING - 1)], *b_img = sB[j & (RING - 1)];
+        const unsigned char *a_img = sA[j % RING], *b_img = sB[j % RING];
         V8 fa[4], fb[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {

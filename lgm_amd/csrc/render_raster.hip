@@ -754,13 +754,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // the first chunk's ids and LDS DMA go out before the per-pixel state loads (bounded by the list length n, a
     // superset of [s0, s1): rows past s1 are staged but never listed or flushed), so their two dependent memory
     // round trips overlap the pixel loads instead of following them
-#ifdef LGM_BWD_W3STAGE
-    // wave 3 stages (and issues no gradient atomics); waves 0-2 convert and flush (their atomics are never waited for)
-    constexpr int SW = 3;
-#else
-    constexpr int SW = 0;
-#endif
-    const bool stager = w == SW;
+    const bool stager = w == 0;  // (wave 3 staging, with waves 0-2 flushing and never waiting for their atomics, measured
+                                 // slower: pool k_render_bwd 608 -> 620 us, profiles/r06/ab_bwd_w3)
     const int s0e = c * TILE_PIX;
     unsigned id_cur = stager && s0e + lane < n ? ids[s0e + lane] : 0u;
     if (stager && s0e + lane < n) stage_dma(S.buf[0], 0, id_cur, (size_t)bv * d.N, b, d.N, gP, gQ, gauss);
@@ -1138,12 +1133,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
         SEC_T(ts_c3);
         SEC_ADD(sec[4], ts_c2, ts_c3);  // barrier + moments -> partials
 #endif
-#ifdef LGM_BWD_W3STAGE
-        if (stager) vm_wait_all();  // the next chunk's rows and ids (only the stager has anything to wait for)
-#else
         // the next chunk's DMA and ids have landed before the atomics below go out (they cannot delay it)
         vm_wait_all();
-#endif
 #ifdef LGM_BWD_STAMPS
         SEC_T(ts_c3a);
         SEC_ADD(sec[5], ts_c3, ts_c3a);  // DMA wait (and any earlier outstanding vector-memory op of this wave)
@@ -1155,13 +1146,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
 #endif
         // flush: lane -> (entry, value) flat, so one global-atomic wave-instruction covers ~6 contiguous 40-B
         // gradient records instead of 64 scattered rows
-#ifdef LGM_BWD_W3STAGE
-        constexpr int FT = 192, FQ = NV;  // waves 0-2 flush, CH * NV items exactly (3 passes at NV = 9)
-        if (w < 3) {
-#else
         constexpr int FT = 256, FQ = NACC;  // flushing threads; items per entry in the lane mapping
         {
-#endif
         int ft = tid;
         // the lane's (entry, partial) indices recomputed per chunk: hoisted out of the chunk loop, their 64-bit
         // per-scene accumulator offsets were spilled, and each reload's vmcnt(0) waited for this flush's earlier atomics

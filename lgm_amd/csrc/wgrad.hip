@@ -36,13 +36,11 @@ typedef __attribute__((ext_vector_type(8))) short s8v;
 
 constexpr int BM = 128, BN = 128;  // output tile (dw rows x columns) of one workgroup
 constexpr int BK = 32;             // K rows per stage (one MFMA K step)
-#ifndef LGM_WGRAD_RING
-#define LGM_WGRAD_RING 4
-#endif
-constexpr int RING = LGM_WGRAD_RING;  // LDS stages; RING - 1 in flight
+constexpr int RING = 4;            // LDS stages; RING - 1 in flight (3 stages at 3 workgroups per CU measured slower:
+                                   // k_wgrad 65 -> 68 us, the larger split's reduce 22.6 -> 32 us, profiles/r06/ab_wgrad_ring)
 constexpr int THREADS = 256;
 constexpr int IMG = BK * 256;      // bytes of one operand's stage image (32 rows x 128 16-bit columns)
-constexpr int WPE = 2 * 4 / RING + (RING == 3 ? 1 : 0);  // workgroups (= waves per SIMD) per CU: 64 KB (ring 4) -> 2, 48 KB -> 3
+constexpr int WPE = 2;             // workgroups (= waves per SIMD) per CU: 64 KB of LDS each
 constexpr int SLOTS = 256 * WPE;   // workgroup slots the split targets
 constexpr int FRAGS = 16;          // 16 x 16 accumulator blocks per wave
 

@@ -41,8 +41,11 @@ constexpr int RING = 4;            // LDS stages; RING - 1 in flight (3 stages a
 constexpr int THREADS = 256;
 constexpr int IMG = BK * 256;      // bytes of one operand's stage image (32 rows x 128 16-bit columns)
 constexpr int WPE = 2;             // workgroups (= waves per SIMD) per CU: 64 KB of LDS each
-constexpr int SLOTS = 256 * WPE;   // workgroup slots the split targets
+// workgroup slots the split targets (one round at 2 per CU). Targeting 256 (one per CU) or 1,024 (two rounds)
+// measured slower at both Linears (bench level qkv 70.8 -> 111 / 72 us, proj 30 -> 41 / 34 us; profiles/r06/wgrad_split)
+constexpr int SLOTS = 256 * WPE;
 constexpr int FRAGS = 16;          // 16 x 16 accumulator blocks per wave
+constexpr int DBT = 8;             // k_wgrad_reduce lanes per bias-gradient row
 
 template <int DT> struct Op;
 template <> struct Op<LGM_ATTN_BF16> { using V8 = bf16x8; static constexpr short ONE = 0x3f80; };
@@ -127,6 +130,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const int s = item / tiles, tile = item - s * tiles, mt = tile / NT, nt = tile - mt * NT;
     const int m0 = mt * BM, n0 = nt * BN;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, wm = w >> 1, wn = w & 1;
+    const int wn_u = __builtin_amdgcn_readfirstlane(w) & 1;  // (wave-uniform copy of wn: a scalar branch)
     const int nst_all = (K + BK - 1) / BK, q = nst_all / S, r = nst_all - q * S;
     const int st0 = s * q + min(s, r), nst = q + (s < r ? 1 : 0);
     const bool want_db = dbpart != nullptr;
@@ -175,9 +179,16 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(WPE))) 
         for (int u = 0; u < 4; u++)
 #pragma unroll
             for (int v = 0; v < 4; v++) acc[4 * u + v] = mfma<DT>(fa[u], fb[v], acc[4 * u + v]);
+        // (static fragment indices under a wave-uniform branch: indexing fa by 2 * wn, a VGPR value to the compiler,
+        // became a ~1,500-instruction select chain per stage and doubled the launch: 30 -> 60 us at the proj level)
         if (want_db && (st0 + j) % NT == nt) {
-            dbacc[0] = mfma<DT>(fa[2 * wn], ones, dbacc[0]);
-            dbacc[1] = mfma<DT>(fa[2 * wn + 1], ones, dbacc[1]);
+            if (wn_u == 0) {
+                dbacc[0] = mfma<DT>(fa[0], ones, dbacc[0]);
+                dbacc[1] = mfma<DT>(fa[1], ones, dbacc[1]);
+            } else {
+                dbacc[0] = mfma<DT>(fa[2], ones, dbacc[0]);
+                dbacc[1] = mfma<DT>(fa[3], ones, dbacc[1]);
+            }
         }
     }
     // fp32 partials in fragment order: one float4 per lane per fragment, 1 KiB per wave-instruction
@@ -193,7 +204,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
 // k_wgrad_reduce: grid (ceil(tiles * 4096 / 256) + [ceil(Mp / 256)]), block 256. One thread per (tile, wave,
 // fragment, lane) float4 position: the S partials summed in split order (up to 16 loads in flight), the 4 values scattered to
-// dw; then (db) one thread per row: the NT * S column-sum partials in order.
+// dw; then (db) DBT threads per row: the NT * S column-sum partials in a fixed order.
 __global__ __launch_bounds__(256) void k_wgrad_reduce(int M, int N, int S, int NT, int tiles,
                                                       const f32x4 *__restrict__ part, const float *__restrict__ dbpart,
                                                       int Mp, float *__restrict__ dw, float *__restrict__ db) {
@@ -222,11 +233,25 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(int M, int N, int S, int N
         return;
     }
     if (!db) return;
-    const long long m = p - ((npos + 255) / 256) * 256;
-    if (m >= M) return;
+    // db: DBT lanes per row (adjacent lanes), each summing a contiguous eighth of the NT * S partials in order (all
+    // its loads in flight), then a fixed xor tree over the DBT lanes: deterministic. (One thread per row summing all
+    // 128 partials of the bench's proj level one load at a time took 34 us.)
+    const long long q = p - ((npos + 255) / 256) * 256;
+    const int m = (int)(q / DBT), part8 = (int)(q % DBT);
+    const int nq = NT * S, per = (nq + DBT - 1) / DBT, q0 = part8 * per, q1 = min(nq, q0 + per);
     float v = 0.f;
-    for (int qq = 0; qq < NT * S; qq++) v += dbpart[(size_t)qq * Mp + m];
-    db[m] = v;
+    if (m < M) {
+        for (int qq = q0; qq < q1; qq += 16) {
+            float t[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) t[u] = qq + u < q1 ? dbpart[(size_t)(qq + u) * Mp + m] : 0.f;
+#pragma unroll
+            for (int u = 0; u < 16; u++) v += t[u];
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < DBT; o <<= 1) v += __shfl_xor(v, o, 64);  // (the same tree in every lane)
+    if (m < M && part8 == 0) db[m] = v;
 }
 
 struct Plan {
@@ -296,7 +321,7 @@ extern "C" int lgm_linear_wgrad(int dtype, int K, int M, int N, const void *dy, 
                                       K, M, N, (const uint16_t *)dy, ld_dy, (const uint16_t *)x, ld_x, P.S, P.NT, part,
                                       dbpart, P.Mp)));
     const long long npos = (long long)P.tiles * 4 * FRAGS * 64;
-    const int rgrid = (int)((npos + 255) / 256) + (db ? (M + 255) / 256 : 0);
+    const int rgrid = (int)((npos + 255) / 256) + (db ? (M * DBT + 255) / 256 : 0);
     LGM_LAUNCH("k_wgrad_reduce", st, (k_wgrad_reduce<<<rgrid, 256, 0, st>>>(M, N, P.S, P.NT, P.tiles, part, dbpart,
                                                                              P.Mp, dw, db)));
     return LGM_OK;

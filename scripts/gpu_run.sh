@@ -12,6 +12,7 @@
 #   benchargs=ARGS       bench.py ARGS once (e.g. "benchargs=--steps 40 --only-pool")
 #   prof                 rocprofv3 --kernel-trace --stats of the default bench + per-grid split, then one rocprofv3
 #                        run per PMC pass of scripts/pmc_passes.txt (counters only with --kernel-trace)
+#   trace=ARGS           rocprofv3 --kernel-trace --stats of bench.py ARGS, split per grid (no counters)
 #   ab[=LIBS]            interleaved A/B of lgm_amd/_lib/variants/lib_*.so (render: bench kernel times + output hashes)
 #   abattn               the same for the attention kernels (scripts/bench_attn.py)
 #   abmva[=LIBS]         bench.py --only-attn per variant library (MVAttention level, attention, cfg4)
@@ -67,6 +68,13 @@ for step in "$@"; do
         rc=$?; echo "pass $i ($line) rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done < scripts/pmc_passes.txt
       python scripts/pmc_summary.py "$OUT/pmc" --json "$OUT/pmc_latest.json" > "$OUT/pmc_summary.txt"; echo "pmc summary rc=$?" ;;
+    trace)  # rocprofv3 kernel trace + stats of bench.py ARGS (no counters), split per grid
+      mkdir -p "$OUT/trace"
+      # shellcheck disable=SC2086
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python bench.py $arg > "$OUT/trace/bench.json" 2> "$OUT/trace/bench.err"
+      rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      python scripts/kernel_stats_by_grid.py "$OUT/trace/run_kernel_trace.csv" > "$OUT/trace/kernel_stats_by_grid.txt"
+      head -40 "$OUT/trace/kernel_stats_by_grid.txt" ;;
     ab)
       OUTAB="$OUT/ab" AB_LIBS="$arg" bash scripts/gpu_ab.sh || exit $? ;;
     abattn)

@@ -15,8 +15,6 @@
 //                      composite key (LDS blocks + global merge stages).
 #include "render_common.h"
 
-#include <type_traits>
-
 namespace lgm {
 namespace {
 
@@ -53,10 +51,7 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 // per workgroup instead of once per view (pool 199 -> 193 us, single scene 40.6 -> 38.8 us; 1 / 2 / 6 views per
 // workgroup measured slower).
 constexpr int BIN_THREADS = 512, BIN_G = BIN_THREADS, BIN_ITERS = 3;
-// Launches that would give fewer binning workgroups than CUs (one view of 50k Gaussians, BASELINE config 2: 98
-// workgroups of 512 on 256 CUs) take 128-thread workgroups instead (391 there): the same per-Gaussian work spread over
-// the chip. Outputs are the same (the tile lists are sorted afterwards; records are per Gaussian).
-constexpr int BIN_THREADS_SMALL = 128;
+constexpr int BIN_HITCAP = BIN_THREADS * 6;  // hit-list capacity (typical: ~4 hits per Gaussian)
 static_assert(BIN_THREADS <= 512, "owner index packs into 9 bits");
 
 // One Gaussian's emit record in LDS (48 B). The tiles a Gaussian can reach are found ROW BY ROW: for the tile row's
@@ -92,10 +87,9 @@ __device__ __forceinline__ int wave_incl_max(int v, int /*lane*/) {
 // the short ones fill the second. One binning workgroup writes it at its end: a counting sort of the tiles on their
 // squared centre distance quantised to min(T, BIN_THREADS) buckets, in LDS (hk: >= that + RS-wave sums ints). Ties
 // take atomic slots -- the order only schedules the sorts, every order gives the same result.
-template <int NT>
 __device__ void center_order(int gx, int T, int *__restrict__ corder, int *hk) {
     const int gy = (T + gx - 1) / gx, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int K = min(T, NT);
+    const int K = min(T, BIN_THREADS);
     const long long maxkey = (long long)(gx - 1) * (gx - 1) + (long long)(gy - 1) * (gy - 1);
     auto key = [&](int t) {
         const int y = t / gx, x = t - y * gx, dx = 2 * x - (gx - 1), dy = 2 * y - (gy - 1);
@@ -104,7 +98,7 @@ __device__ void center_order(int gx, int T, int *__restrict__ corder, int *hk) {
     __syncthreads();  // (hk is the binning histogram's LDS)
     if (tid < K) hk[tid] = 0;
     __syncthreads();
-    for (int t = tid; t < T; t += NT) atomicAdd(&hk[key(t)], 1);
+    for (int t = tid; t < T; t += BIN_THREADS) atomicAdd(&hk[key(t)], 1);
     __syncthreads();
     const int v = tid < K ? hk[tid] : 0;
     const int incl = wave_incl_scan(v, lane);
@@ -115,11 +109,11 @@ __device__ void center_order(int gx, int T, int *__restrict__ corder, int *hk) {
     __syncthreads();
     if (tid < K) hk[tid] = run;
     __syncthreads();
-    for (int t = tid; t < T; t += NT) corder[atomicAdd(&hk[key(t)], 1)] = t;
+    for (int t = tid; t < T; t += BIN_THREADS) corder[atomicAdd(&hk[key(t)], 1)] = t;
 }
 
-template <int MODE, int NT>  // NT: threads = Gaussians per workgroup (NT, or NT_SMALL)
-__global__ __launch_bounds__(NT) void k_bin(Dims d, const float *__restrict__ gauss, const float *__restrict__ views,
+template <int MODE>
+__global__ __launch_bounds__(BIN_THREADS) void k_bin(Dims d, const float *__restrict__ gauss, const float *__restrict__ views,
                                                      const float *__restrict__ projs, float4 *__restrict__ gP,
                                                      float4 *__restrict__ gQ,
                                                      uint2 *__restrict__ rects, int *__restrict__ radii_out,
@@ -128,10 +122,10 @@ __global__ __launch_bounds__(NT) void k_bin(Dims d, const float *__restrict__ ga
                                                      unsigned long long *__restrict__ misc, float *__restrict__ accum,
                                                      int *__restrict__ corder) {
     extern __shared__ int hist[];  // [T] per-tile hit counts, [T] reserved global bases, [T] fallback cursors
-    __shared__ BinRec srec[NT];
-    __shared__ int sHead[NT], sExcl[NT];
-    __shared__ unsigned sHit[(NT * 6)];         // owner | tile << 9
-    __shared__ unsigned short sRank[(NT * 6)];  // rank of the hit within its tile (this workgroup)
+    __shared__ BinRec srec[BIN_THREADS];
+    __shared__ int sHead[BIN_THREADS], sExcl[BIN_THREADS];
+    __shared__ unsigned sHit[BIN_HITCAP];         // owner | tile << 9
+    __shared__ unsigned short sRank[BIN_HITCAP];  // rank of the hit within its tile (this workgroup)
     __shared__ int s_nhit;
     __shared__ unsigned long long s_tot[2];
     const int T = d.T, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -164,7 +158,7 @@ __global__ __launch_bounds__(NT) void k_bin(Dims d, const float *__restrict__ ga
     // BIN_ITERS batches per workgroup, one after the other: fewer, longer workgroups (2 per CU: 106 VGPRs at 8 waves
     // per workgroup) fit the single scene's launch into one round of residency. The batches are views of the same
     // Gaussians, whose rows are loaded once.
-    const int i = blockIdx.x * NT + tid;
+    const int i = blockIdx.x * BIN_G + tid;
     float g[14];
     if (i < d.N) load_gaussian(gauss + ((size_t)b * d.N + i) * 14, g);
     for (int it = 0; it < BIN_ITERS; it++) {
@@ -173,7 +167,7 @@ __global__ __launch_bounds__(NT) void k_bin(Dims d, const float *__restrict__ ga
     cur = tile_count + (size_t)bv * T;
     if (tid == 0) s_nhit = 0;
     if (lds)
-        for (int t = tid; t < T; t += NT) hist[t] = 0;
+        for (int t = tid; t < T; t += BIN_THREADS) hist[t] = 0;
     // ---- preprocess, one Gaussian per thread
     Geo o;
     bool vis = false;
@@ -287,7 +281,7 @@ __global__ __launch_bounds__(NT) void k_bin(Dims d, const float *__restrict__ ga
                 const int rk = atomicAdd(&hist[t], 1);
                 if (MODE != COUNT) {
                     const int slot = slot0 + k;
-                    if (slot < (NT * 6)) {
+                    if (slot < BIN_HITCAP) {
                         sHit[slot] = (unsigned)owner | ((unsigned)t << 9);
                         sRank[slot] = (unsigned short)rk;
                     }
@@ -307,7 +301,7 @@ __global__ __launch_bounds__(NT) void k_bin(Dims d, const float *__restrict__ ga
     if (lds) {
         __syncthreads();
         phase(1);
-        for (int t = tid; t < T; t += NT) {
+        for (int t = tid; t < T; t += BIN_THREADS) {
             const int c = hist[t];
             if (c) {
                 if (MODE == COUNT) atomicAdd(&cur[t], c);
@@ -319,8 +313,8 @@ __global__ __launch_bounds__(NT) void k_bin(Dims d, const float *__restrict__ ga
         phase(2);
         if (MODE != COUNT) {
             const int H = s_nhit;
-            if (H <= (NT * 6)) {
-                for (int h = tid; h < H; h += NT) {
+            if (H <= BIN_HITCAP) {
+                for (int h = tid; h < H; h += BIN_THREADS) {
                     const unsigned e2 = sHit[h];
                     const int t = (int)(e2 >> 9);
                     pairs[dest(t, hbase[t] + sRank[h])] = srec[e2 & 511u].key;
@@ -346,7 +340,7 @@ __global__ __launch_bounds__(NT) void k_bin(Dims d, const float *__restrict__ ga
         atomicAdd(&misc[0], s_tot[0]);
         atomicAdd(&misc[1], s_tot[1]);
     }
-    if (corder && blockIdx.x == 0 && blockIdx.y == 0) center_order<NT>(d.gx, T, corder, hist);
+    if (corder && blockIdx.x == 0 && blockIdx.y == 0) center_order(d.gx, T, corder, hist);
 }
 
 // k_scan: one workgroup of 1024 threads; exclusive scan of the M tile counts -> tile_start[0..M].
@@ -860,35 +854,24 @@ int launch_binning(const Dims &d, const float *gaussians, const float *cam_view,
     // k_sort's centre-first tile table (the first T ints of the order buffer; the binning histogram's 3T ints of LDS
     // hold its counting sort)
     int *corder = lds && d.T >= 8 ? (int *)(ws + L.order) : nullptr;
-    const int vg = d.B * ((d.V + BIN_ITERS - 1) / BIN_ITERS);
-    // (the diagnostic timeline has room for the 512-thread grid only: launches with counters keep it)
-    const bool small = !d.counters && (long long)((d.N + BIN_G - 1) / BIN_G) * vg < 256;
-    const int nt = small ? BIN_THREADS_SMALL : BIN_THREADS;
-    dim3 grid((d.N + nt - 1) / nt, vg);
-    auto kb = [&](auto mode_tag) {
-        constexpr int MD = decltype(mode_tag)::value;
-        return small ? k_bin<MD, BIN_THREADS_SMALL> : k_bin<MD, BIN_THREADS>;
-    };
+    dim3 grid((d.N + BIN_G - 1) / BIN_G, d.B * ((d.V + BIN_ITERS - 1) / BIN_ITERS));
     if (d.N > 0) {
         if (count_only || !L.slot) {
-            LGM_LAUNCH("k_bin_count", st, (kb(std::integral_constant<int, COUNT>{})<<<grid, nt, lds, st>>>(
-                                              d, gaussians, cam_view, cam_view_proj, gP, gQ, rects, nullptr, tcount,
-                                              tstart, pairs, 0, misc, accum, nullptr)));
+            LGM_LAUNCH("k_bin_count", st, (k_bin<COUNT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
+                       gP, gQ, rects, nullptr, tcount, tstart, pairs, 0, misc, accum, nullptr)));
         }
         if (!count_only) {
             if (L.slot) {
-                LGM_LAUNCH("k_bin", st, (kb(std::integral_constant<int, EMIT_SLOT>{})<<<grid, nt, lds, st>>>(
-                                            d, gaussians, cam_view, cam_view_proj, gP, gQ, rects, radii_out, tcount,
-                                            tstart, pairs, (long long)d.N, misc, accum, corder)));
+                LGM_LAUNCH("k_bin", st, (k_bin<EMIT_SLOT><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view, cam_view_proj,
+                           gP, gQ, rects, radii_out, tcount, tstart, pairs, (long long)d.N, misc, accum, corder)));
             } else {
                 LGM_LAUNCH("k_scan", st, (k_scan<<<1, 1024, 0, st>>>(tcount, (int)M, tstart)));
                 if (hipMemsetAsync(ws + L.tile_count, 0, L.misc + 64 - L.tile_count, st) != hipSuccess) {
                     set_error("hipMemsetAsync failed");
                     return LGM_E_HIP;
                 }
-                LGM_LAUNCH("k_bin", st, (kb(std::integral_constant<int, EMIT_PACKED>{})<<<grid, nt, lds, st>>>(
-                                            d, gaussians, cam_view, cam_view_proj, gP, gQ, rects, radii_out, tcount,
-                                            tstart, pairs, 0, misc, accum, corder)));
+                LGM_LAUNCH("k_bin", st, (k_bin<EMIT_PACKED><<<grid, BIN_THREADS, lds, st>>>(d, gaussians, cam_view,
+                           cam_view_proj, gP, gQ, rects, radii_out, tcount, tstart, pairs, 0, misc, accum, corder)));
             }
             LGM_LAUNCH("k_sort", st, (k_sort<<<(unsigned)M, RS_THREADS, RS_LDS, st>>>(
                                          (int)M, L.slot ? (long long)d.N : -1LL, tstart, tcount, pairs, d.counters,

@@ -35,11 +35,15 @@ typedef short s4v __attribute__((__vector_size__(8)));
 typedef __attribute__((ext_vector_type(8))) short s8v;
 
 constexpr int BM = 128, BN = 128;  // output tile (dw rows x columns) of one workgroup
-constexpr int BK = 32;             // K rows per stage (one MFMA K step)
-constexpr int RING = 4;            // LDS stages; RING - 1 in flight (3 stages at 3 workgroups per CU measured slower:
+#ifndef LGM_WGRAD_BK
+#define LGM_WGRAD_BK 32
+#endif
+constexpr int BK = LGM_WGRAD_BK;   // K rows per stage (BK / 32 MFMA K steps)
+constexpr int DPS = BK / 8;        // LDS-DMA pieces per wave per stage (both operands)
+constexpr int RING = BK == 32 ? 4 : 2;            // LDS stages; RING - 1 in flight (3 stages at 3 workgroups per CU measured slower:
                                    // k_wgrad 65 -> 68 us, the larger split's reduce 22.6 -> 32 us, profiles/r06/ab_wgrad_ring)
 constexpr int THREADS = 256;
-constexpr int IMG = BK * 256;      // bytes of one operand's stage image (32 rows x 128 16-bit columns)
+constexpr int IMG = BK * 256;      // bytes of one operand's stage image (BK rows x 128 16-bit columns)
 constexpr int WPE = 2;             // workgroups (= waves per SIMD) per CU: 64 KB of LDS each
 // workgroup slots the split targets (one round at 2 per CU). Targeting 256 (one per CU) or 1,024 (two rounds)
 // measured slower at both Linears (bench level qkv 70.8 -> 111 / 72 us, proj 30 -> 41 / 34 us; profiles/r06/wgrad_split)
@@ -82,8 +86,8 @@ __device__ __forceinline__ void stage(const uint16_t *__restrict__ src, long lon
                                       int ncols, unsigned char *img) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const int p = 2 * w + q, row = 4 * p + (lane >> 4), slot = lane & 15;
+    for (int q = 0; q < BK / 16; q++) {
+        const int p = (BK / 16) * w + q, row = 4 * p + (lane >> 4), slot = lane & 15;
         const int lc = (slot >> 1) ^ (row & 7);                // logical 32-B chunk stored at physical chunk slot / 2
         const int col = min(col0 + 16 * lc + 8 * (slot & 1), ncols - 8);
         const uint16_t *s = src + (long long)(k0 + row) * ld + col;
@@ -163,31 +167,35 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(WPE))) 
     for (int j = 0; j < nst; j++) {
         // stage j has landed once at most the DMAs of the stages issued after it (4 per stage per wave) are pending
         const int ahead = min(nst - 1, j + RING - 2) - j;
-        if (ahead >= 2) vm_wait<8>();
-        else if (ahead == 1) vm_wait<4>();
+        if (ahead >= 2) vm_wait<2 * DPS>();
+        else if (ahead == 1) vm_wait<DPS>();
         else vm_wait<0>();
         __syncthreads();  // every wave's copies of stage j have landed; slot (j - 1) % RING is free
         if (j + RING - 1 < nst) issue(j + RING - 1);
-        const unsigned char *a_img = sA[j % RING], *b_img = sB[j % RING];
-        V8 fa[4], fb[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            fa[u] = frag<DT>(a_img, 4 * wm + u, lane);
-            fb[u] = frag<DT>(b_img, 4 * wn + u, lane);
-        }
+        for (int kk = 0; kk < BK / 32; kk++) {  // the stage's 32-row K steps
+            const unsigned char *a_img = sA[j % RING] + kk * 32 * 256, *b_img = sB[j % RING] + kk * 32 * 256;
+            V8 fa[4], fb[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++)
+            for (int u = 0; u < 4; u++) {
+                fa[u] = frag<DT>(a_img, 4 * wm + u, lane);
+                fb[u] = frag<DT>(b_img, 4 * wn + u, lane);
+            }
 #pragma unroll
-            for (int v = 0; v < 4; v++) acc[4 * u + v] = mfma<DT>(fa[u], fb[v], acc[4 * u + v]);
-        // (static fragment indices under a wave-uniform branch: indexing fa by 2 * wn, a VGPR value to the compiler,
-        // became a ~1,500-instruction select chain per stage and doubled the launch: 30 -> 60 us at the proj level)
-        if (want_db && (st0 + j) % NT == nt) {
-            if (wn_u == 0) {
-                dbacc[0] = mfma<DT>(fa[0], ones, dbacc[0]);
-                dbacc[1] = mfma<DT>(fa[1], ones, dbacc[1]);
-            } else {
-                dbacc[0] = mfma<DT>(fa[2], ones, dbacc[0]);
-                dbacc[1] = mfma<DT>(fa[3], ones, dbacc[1]);
+            for (int u = 0; u < 4; u++)
+#pragma unroll
+                for (int v = 0; v < 4; v++) acc[4 * u + v] = mfma<DT>(fa[u], fb[v], acc[4 * u + v]);
+            // (static fragment indices under a wave-uniform branch: indexing fa by 2 * wn, a VGPR value to the
+            // compiler, became a ~1,500-instruction select chain per stage and doubled the launch: 30 -> 60 us at the
+            // proj level)
+            if (want_db && ((st0 + j) * (BK / 32) + kk) % NT == nt) {
+                if (wn_u == 0) {
+                    dbacc[0] = mfma<DT>(fa[0], ones, dbacc[0]);
+                    dbacc[1] = mfma<DT>(fa[1], ones, dbacc[1]);
+                } else {
+                    dbacc[0] = mfma<DT>(fa[2], ones, dbacc[0]);
+                    dbacc[1] = mfma<DT>(fa[3], ones, dbacc[1]);
+                }
             }
         }
     }

@@ -11,10 +11,10 @@
 //     read (ds_read_b64_tr_b16): a 32-row stage of dy and of x is copied into LDS by LDS DMA (global_load_lds, no
 //     staging registers) as 256-B rows whose 32-B chunks are XOR-swizzled by the row (chunk c of row r at c ^ (r & 7)),
 //     which puts the 8 rows of every 32-lane half of a transposed read on distinct banks;
-//   * a 4-stage LDS ring with three stages in flight (counted vmcnt waits), one barrier per stage (fragments of stage
-//     j + 1 read during stage j's MFMAs, software-pipelined at 210 VGPRs, measured slower: 59.7 -> 64-65 us per
-//     launch, profiles/r06/ab_wgrad_pipe);
-//   * 4 waves per workgroup in 2 x 2, each a 64 x 64 block = 16 v_mfma_f32_16x16x32 per stage;
+//   * 64-row stages, double-buffered (the next stage's DMA in flight during the current one's MFMAs), one barrier per
+//     stage (fragments of stage j + 1 read during stage j's MFMAs, software-pipelined at 210 VGPRs, measured slower
+//     with 32-row stages: 59.7 -> 64-65 us per launch, profiles/r06/ab_wgrad_pipe);
+//   * 4 waves per workgroup in 2 x 2, each a 64 x 64 block = 16 v_mfma_f32_16x16x32 per 32-row K step;
 //   * db on the same MFMAs: the dy fragment times a ones operand gives the column sums; each workgroup adds the
 //     stages whose index is congruent to its column tile (so the work is spread over the column tiles), and the
 //     reduce kernel sums those partials in a fixed order too.
@@ -35,13 +35,13 @@ typedef short s4v __attribute__((__vector_size__(8)));
 typedef __attribute__((ext_vector_type(8))) short s8v;
 
 constexpr int BM = 128, BN = 128;  // output tile (dw rows x columns) of one workgroup
-#ifndef LGM_WGRAD_BK
-#define LGM_WGRAD_BK 32
-#endif
-constexpr int BK = LGM_WGRAD_BK;   // K rows per stage (BK / 32 MFMA K steps)
+// K rows per stage: two 32-row MFMA K steps per barrier, double-buffered (one stage in flight). Against 32-row stages in
+// a 4-deep ring (three in flight): qkv 72.5 / 73.7 -> 65.7 / 65.8 us, proj (bias) 32.0 / 32.4 -> 29.4 / 30.2 us at the
+// bench level (profiles/r06/ab_wgrad_bk64): half the barriers and waits per MFMA
+constexpr int BK = 64;
 constexpr int DPS = BK / 8;        // LDS-DMA pieces per wave per stage (both operands)
-constexpr int RING = BK == 32 ? 4 : 2;            // LDS stages; RING - 1 in flight (3 stages at 3 workgroups per CU measured slower:
-                                   // k_wgrad 65 -> 68 us, the larger split's reduce 22.6 -> 32 us, profiles/r06/ab_wgrad_ring)
+constexpr int RING = BK == 32 ? 4 : 2;  // LDS stages; RING - 1 in flight (with 32-row stages, 3 stages at 3 workgroups
+                                        // per CU measured slower: k_wgrad 65 -> 68 us, profiles/r06/ab_wgrad_ring)
 constexpr int THREADS = 256;
 constexpr int IMG = BK * 256;      // bytes of one operand's stage image (BK rows x 128 16-bit columns)
 constexpr int WPE = 2;             // workgroups (= waves per SIMD) per CU: 64 KB of LDS each

@@ -1,5 +1,6 @@
 """Hashes of every render output for the library in LGM_AMD_LIB (or the default): bench.py's pool (fwd + bwd,
-deterministic gradients), a cfg5-like fused-loss render at 512^2, and a ragged small case -- so kernel variants that
+deterministic gradients), a cfg5-like fused-loss render at 512^2, a ragged small case and
+one 256^2 view (the launches of at most 256 tiles: k_render_fwd's small-launch form) -- so kernel variants that
 must be bitwise equal can be compared across child processes (scripts/gpu_ab.sh prints them per variant)."""
 import hashlib
 import json
@@ -21,7 +22,8 @@ def h(t):
 
 dev = torch.device("cuda:0")
 out = {}
-for name, (B, N, V, S, seed) in {"pool": (8, 100000, 6, 256, 2), "ragged": (2, 3000, 3, 72, 5)}.items():
+for name, (B, N, V, S, seed) in {"pool": (8, 100000, 6, 256, 2), "ragged": (2, 3000, 3, 72, 5),
+                                    "one_view": (1, 50000, 1, 256, 3)}.items():
     r = GaussianRenderer(Options(output_size=S))
     g = synthetic_gaussians(B, N, seed=seed).to(dev).requires_grad_(True)
     cv, cvp, cp = (t[None].expand(B, *t.shape).contiguous().to(dev) for t in orbit_cameras(V, elevation=10.0))

@@ -373,6 +373,47 @@ def test_headline_pool_batched_equals_per_scene(cuda, oracle_mod):
     _check(oracle_mod, out, g0, c0, cp0, R, R, bg, d_m, d_alpha[0:1], name="pool scene 0 (production path)")
 
 
+@pytest.mark.parametrize("H,W,N,seed", [(256, 256, 50_000, 3), (136, 200, 20_000, 4)])
+def test_small_launch_form_bitwise(cuda, H, W, N, seed):
+    """Launches of at most 256 tiles (one 256^2 view: BASELINE config 2) take k_render_fwd's small-launch form (8
+    entries per step at 2 waves per SIMD), larger launches the 4-entry form at 7. The same (scene, view) rendered alone
+    (256 / 117 tiles) and as every scene of a 6-scene batch (1,536 / 702 tiles): image, depth, alpha, n_contrib and
+    final T bitwise equal, the backward's gradients bitwise equal in deterministic mode (so the forward left the same
+    checkpoints and list bounds), and with the fused loss the same image."""
+    from lgm_amd.gs import rasterize
+    g = synthetic_gaussians(1, N, seed=seed)
+    cv, cvp, _ = orbit_cameras(1)
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(1, 1, H, W, seed=seed + 100)
+    d_dep = torch.randn(1, 1, 1, H, W, generator=torch.Generator().manual_seed(seed + 200))
+    gen = torch.Generator().manual_seed(seed + 300)
+    gt_img, gt_mask = torch.rand(1, 1, 3, H, W, generator=gen), (torch.rand(1, 1, 1, H, W, generator=gen) > 0.3).float()
+
+    def rep(t, B):
+        return t.expand(B, *t.shape[1:]).contiguous().to(cuda)
+
+    def run(B):
+        gd = rep(g, B).requires_grad_(True)
+        img, dep, alp = rasterize(gd, rep(cv[None], B), rep(cvp[None], B), bg.to(cuda), TAN, TAN, H, W, clamp=True,
+                                  deterministic=True)
+        torch.autograd.backward([img, dep, alp], [rep(d_img, B), rep(d_dep, B), rep(d_alpha, B)])
+        nc, ft = (forward_state(rep(g, B), rep(cv[None], B), rep(cvp[None], B), TAN, TAN, H, W)[k]
+                  for k in ("n_contrib", "final_T"))
+        with torch.no_grad():
+            li = rasterize(rep(g, B), rep(cv[None], B), rep(cvp[None], B), bg.to(cuda), TAN, TAN, H, W, clamp=True,
+                           gt_images=rep(gt_img, B), gt_masks=rep(gt_mask, B))
+        torch.cuda.synchronize()
+        return [img.detach(), dep.detach(), alp.detach(), gd.grad, torch.as_tensor(nc), torch.as_tensor(ft), li[0],
+                li[3]]
+
+    alone, batched = run(1), run(6)
+    names = ["image", "depth", "alpha", "gradient", "n_contrib", "final_T", "image (fused loss)"]
+    for s in range(6):
+        for nm, a, b in zip(names, alone, batched):
+            assert torch.equal(a[0].cpu(), b[s].cpu()), f"{H}x{W} scene {s}: {nm} differs small vs batched form"
+    # the fused loss terms: one view vs six copies of it (sums in a different order: float tolerance)
+    assert torch.allclose(alone[7].cpu(), batched[7].cpu(), rtol=1e-5, atol=0)
+
+
 def test_deterministic_checkpoint_split_independent_of_batch(cuda):
     """Deterministic mode on a scene whose tiles walk many chunks (72^2, long lists: the shared checkpoint pool
     would run out): the split of each tile's walk into backward work items follows the tile's own checkpoint quota,

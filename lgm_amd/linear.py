@@ -63,7 +63,11 @@ def _supported(x: torch.Tensor, weight: torch.Tensor, dt) -> bool:
 
 def linear(x: torch.Tensor, lin: torch.nn.Linear) -> torch.Tensor:
     """lin(x), with the HIP weight gradient where the Linear runs in 16 bits on the GPU: under bf16 / fp16 autocast,
-    or on a 16-bit module without autocast. Anything else (fp32, CPU tensors, widths not a multiple of 8) is lin(x)."""
+    or on a 16-bit module without autocast. Anything else (fp32, CPU tensors, widths not a multiple of 8) is lin(x),
+    and so is a call that records no graph (inference: no weight gradient to compute, and the autograd Function's
+    host cost per call -- with its own weight cast -- would only slow the launch stream of LGM's 16-block forward)."""
+    if not (torch.is_grad_enabled() and (x.requires_grad or lin.weight.requires_grad)):
+        return lin(x)
     if x.is_cuda and torch.is_autocast_enabled("cuda"):
         dt = torch.get_autocast_dtype("cuda")
     elif x.dtype in _CODES and lin.weight.dtype == x.dtype:

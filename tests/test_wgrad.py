@@ -111,6 +111,26 @@ def test_linear16_matches_torch_autocast(cuda, bias):
 
 
 @pytest.mark.gpu
+def test_linear16_inference_is_plain_linear(cuda, monkeypatch):
+    """Without a graph to record (no_grad, or nothing requiring grad) linear() is lin(x) itself: bitwise torch's
+    autocast output, and the autograd Function (its host cost and weight cast per call) is never entered."""
+    from lgm_amd import linear as LN
+
+    def boom(*a, **k):
+        raise AssertionError("_Linear16 used without a graph")
+
+    lin = torch.nn.Linear(512, 1536).to(cuda)
+    x = torch.randn(2, 256, 512, device=cuda)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ref = lin(x)
+        monkeypatch.setattr(LN._Linear16, "apply", boom)
+        with torch.no_grad():
+            assert torch.equal(LN.linear(x, lin), ref)
+        lin.requires_grad_(False)
+        assert torch.equal(LN.linear(x, lin), ref)
+
+
+@pytest.mark.gpu
 def test_mvattention_uses_native_wgrad(cuda):
     """MVAttention under bf16 autocast (the bench's level shape, 1 object): k_wgrad runs for both Linears, and the
     parameter gradients match the upstream autograd path (native_wgrad = False) to torch's bf16 rounding."""

@@ -17,6 +17,12 @@
 #   abattn               the same for the attention kernels (scripts/bench_attn.py)
 #   abmva[=LIBS]         bench.py --only-attn per variant library (MVAttention level, attention, cfg4)
 #   py=SCRIPT [ARGS]     python SCRIPT ARGS (a diagnostic under scripts/), output to $OUT/<script>.log
+#   tracepy=SCRIPT [ARGS]  rocprofv3 --kernel-trace --stats of python SCRIPT ARGS, split per grid (every kernel the
+#                        script launches, library GEMMs and torch's own included)
+#   pmcpy=SCRIPT [ARGS]  one rocprofv3 counter run per line of $PASSES (default scripts/pmc_passes.txt) over python
+#                        SCRIPT ARGS (e.g. scripts/probe_cfg2.py with PASSES=scripts/pmc_passes_cfg2.txt), summarised
+#   abwgrad=NAMES        per variant library lib_NAME.so: the weight-gradient tests, then scripts/bench_wgrad.py in
+#                        two interleaved rounds
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=${OUT:-gpurun_out/run}
 mkdir -p "$OUT"
@@ -86,6 +92,34 @@ for step in "$@"; do
       set -- $arg; s=$1; shift
       timeout -k 10 600 python -u "$s" "$@" > "$OUT/$(basename "$s" .py).log" 2>&1
       rc=$?; echo "$s rc=$rc"; tail -5 "$OUT/$(basename "$s" .py).log"; [ $rc -eq 0 ] || exit $rc ;;
+    tracepy)
+      mkdir -p "$OUT/tracepy"
+      # shellcheck disable=SC2086
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/tracepy" -o run --output-format csv -- python $arg > "$OUT/tracepy/run.log" 2>&1
+      rc=$?; echo "tracepy rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      python scripts/kernel_stats_by_grid.py "$OUT/tracepy/run_kernel_trace.csv" > "$OUT/tracepy/kernel_stats_by_grid.txt"
+      head -30 "$OUT/tracepy/kernel_stats_by_grid.txt" ;;
+    pmcpy)
+      mkdir -p "$OUT/pmcpy"
+      i=0
+      while read -r line; do
+        [ -z "$line" ] && continue
+        i=$((i+1))
+        # shellcheck disable=SC2086
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $line -d "$OUT/pmcpy/p$i" -o run --output-format csv -- python $arg > "$OUT/pmcpy/p$i.log" 2>&1
+        rc=$?; echo "pass $i ($line) rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done < "${PASSES:-scripts/pmc_passes.txt}"
+      python scripts/pmc_summary.py "$OUT/pmcpy" > "$OUT/pmcpy/summary.txt"; echo "pmc summary rc=$?" ;;
+    abwgrad)
+      mkdir -p "$OUT/wgab"
+      for v in $arg; do
+        LGM_AMD_LIB=$PWD/lgm_amd/_lib/variants/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_wgrad.py -m gpu -q --timeout 120 --timeout-method thread > "$OUT/wgab/t_$v.log" 2>&1
+        rc=$?; echo "$v tests: $(tail -1 "$OUT/wgab/t_$v.log")"; [ $rc -eq 0 ] || exit $rc
+      done
+      for r in 1 2; do for v in $arg; do
+        LGM_AMD_LIB=$PWD/lgm_amd/_lib/variants/lib_$v.so timeout -k 10 120 python scripts/bench_wgrad.py > "$OUT/wgab/${v}_r$r.jsonl" 2>&1 || exit $?
+        echo "$v r$r"; grep '^{' "$OUT/wgab/${v}_r$r.jsonl"
+      done; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -9,7 +9,7 @@ from lgm_amd import _native
 
 # K, M, N, ld_dy (0: M), bias -- the bench's MVAttention level (8 objects x 4 views x 32^2 tokens, C = 512: qkv and
 # proj), LGM 'big' cfg4 levels (K = 9,600 / 2,400 / 600 tokens, C = 512 / 1024), and ragged edges: K not a multiple
-# of the 32-row stage, M / N not multiples of the 128 tile, K = 0, a strided dy (a column slice of a wider tensor)
+# of the 64-row stage, M / N not multiples of the 128 tile, K = 0, a strided dy (a column slice of a wider tensor)
 WG_CASES = [(32768, 1536, 512, 0, False), (32768, 512, 512, 0, True), (9600, 1536, 512, 0, False),
             (2400, 3072, 1024, 0, False), (600, 1024, 1024, 0, True), (1234, 200, 136, 0, True), (33, 8, 8, 0, True),
             (0, 64, 64, 0, True), (777, 96, 40, 160, True), (5, 24, 16, 0, False)]

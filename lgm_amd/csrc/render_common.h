@@ -95,8 +95,14 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     L.n_contrib = take(BV * P * 4);
     L.wlast = take(BV * T * 16);  // per tile: the four waves' largest last contributor (forward -> backward)
     L.cfin = take(BV * P * 16);  // per-pixel pre-background colour and depth totals (forward -> backward)
-    // backward checkpoints (k_render_fwd -> k_render_bwd): 2 per tile on average, 5 planes of 256 floats each
-    L.ck_region = (int)((2 * BV * T + 7) / 8);
+    // backward checkpoints (k_render_fwd -> k_render_bwd), 5 planes of 256 floats each, in 8 regional pools (a
+    // region is one eighth of the launch's tiles). k_render_bwd launches one workgroup per slot, and an unused slot's
+    // workgroup still pays a dispatch and a counter round trip before it exits: at 2 slots per tile the pool (8 scenes,
+    // ~0.53 used per tile) left 18k such workgroups and cost k_render_bwd ~15 us. A region holds min(2 per tile,
+    // 0.75 per tile + 256): the 8-scene pool 1,408 per region (its busiest uses ~860), one cfg3 scene keeps 2 per
+    // tile (384: its central regions need ~1 per tile), BASELINE config 2 keeps 64 (profiles/r06/ab_bwd_ckcap,
+    // abfull_cap). A full region leaves the rest of a tile's walk to its last checkpointed item (slower, same result).
+    L.ck_region = (int)std::min((2 * BV * T + 7) / 8, (3 * BV * T / 4 + 7) / 8 + 256);
     L.ck_slots = det ? 0 : 8 * L.ck_region;
     L.ck = take((size_t)L.ck_slots * 5 * TILE_PIX * 4);
     L.cklist = take((size_t)L.ck_slots * 8);

@@ -27,6 +27,7 @@ int check_common(int B, int V, int N, int H, int W, const void *g, const void *c
     d.gy = (H + lgm::BY - 1) / lgm::BY;
     d.T = d.gx * d.gy;
     d.BV = B * V;
+    d.ck_shift = lgm::ck_shift_for((size_t)d.BV * d.T);
     d.tanx = tanx; d.tany = tany;
     d.fx = W / (2.0f * tanx);
     d.fy = H / (2.0f * tany);

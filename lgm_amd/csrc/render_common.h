@@ -74,6 +74,18 @@ struct Layout {
 // det (LGM_RENDER_DETERMINISTIC): the per-view gradient accumulators are int64 fixed point (data-scaled units, see
 // render_raster.hip det_norm) instead of fp32: integer atomics commute, so the backward's sums do not depend on the
 // order of its work items.
+// Backward work items span 2^ck_shift staged forward chunks (of TILE_PIX entries): 2 chunks for launches of at least
+// CK_LONG_TILES tiles, where the many short checkpoint items run at the end of k_render_bwd at about half its slots
+// (each workgroup hand-over idles a slot for a few us); one for smaller launches, whose head items already exceed
+// one residency round. Pool (12,288 tiles): k_render_bwd 599 -> 588 us and k_render_fwd -6 us (fewer checkpoints);
+// one cfg3 scene (1,536 tiles) with 2: bwd 92.7 -> 102.8 us (profiles/r06/ab_bwd_cks).
+constexpr size_t CK_LONG_TILES = 4096;
+#ifdef LGM_CK_SHIFT0  // (A/B: one chunk per item at every size)
+__host__ __device__ __forceinline__ int ck_shift_for(size_t) { return 0; }
+#else
+__host__ __device__ __forceinline__ int ck_shift_for(size_t tiles) { return tiles >= CK_LONG_TILES ? 1 : 0; }
+#endif
+
 inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capacity, bool det = false) {
     const size_t BV = (size_t)B * V, T = (size_t)((W + BX - 1) / BX) * ((H + BY - 1) / BY), P = (size_t)H * W;
     Layout L;
@@ -102,7 +114,7 @@ inline Layout make_layout(int B, int V, int N, int H, int W, long long pair_capa
     // 0.75 per tile + 256): the 8-scene pool 1,408 per region (its busiest uses ~860), one cfg3 scene keeps 2 per
     // tile (384: its central regions need ~1 per tile), BASELINE config 2 keeps 64 (profiles/r06/ab_bwd_ckcap,
     // abfull_cap). A full region leaves the rest of a tile's walk to its last checkpointed item (slower, same result).
-    L.ck_region = (int)std::min((2 * BV * T + 7) / 8, (3 * BV * T / 4 + 7) / 8 + 256);
+    L.ck_region = (int)std::min((2 * BV * T + 7) / 8, ((3 * BV * T / 4) >> ck_shift_for(BV * T)) / 8 + 1 + 256);
     L.ck_slots = det ? 0 : 8 * L.ck_region;
     L.ck = take((size_t)L.ck_slots * 5 * TILE_PIX * 4);
     L.cklist = take((size_t)L.ck_slots * 8);
@@ -122,6 +134,7 @@ struct Dims {
     unsigned long long *counters;  // this call's device work counters (lgm_diag.render_counters), or null
     int det_lim_log2;              // lgm_diag.det_limit_log2 (test hook; 0 = the derived bound)
     int options;                   // per-call LGM_RENDER_* bits (NO_CULL, CLAMP_IMAGE, FUSED_LOSS, DETERMINISTIC)
+    int ck_shift;                  // backward work items span 2^ck_shift forward chunks (ck_shift_for(BV * T))
     // LGM_RENDER_FUSED_LOSS (core/models.py:138-160): ground truth [BV,3,P] / [BV,P], the per-tile loss partials
     // (forward) and the gradients of the two MSE terms (backward)
     const float *gt_img, *gt_mask;

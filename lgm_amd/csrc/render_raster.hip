@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FU == FWD_F
         // chunk's compositing to complete before the next wait
         if (tid == 0) {
             ck_slot = -1;
-            if (b0 + TILE_PIX < n && !det_ck) {
+            if (b0 + TILE_PIX < n && !det_ck && ((c + 1) & ((1 << d.ck_shift) - 1)) == 0) {
                 const unsigned l = atomicAdd(&ckctr[ck_reg], 1u);
                 if (l < (unsigned)ck_region) ck_slot = (int)l * 8 + ck_reg;
             }
@@ -306,8 +306,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FU == FWD_F
                 cp[3 * TILE_PIX] = C2;
                 cp[4 * TILE_PIX] = D;
                 if (tid == 0) {
-                    cklist[sl] = make_int2(tile, c);
-                    ck_written = c;
+                    cklist[sl] = make_int2(tile, c >> d.ck_shift);
+                    ck_written = c >> d.ck_shift;
                 }
             }
         }
@@ -783,7 +783,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     // round trips overlap the pixel loads instead of following them
     const bool stager = w == 0;  // (wave 3 staging, with waves 0-2 flushing and never waiting for their atomics, measured
                                  // slower: pool k_render_bwd 608 -> 620 us, profiles/r06/ab_bwd_w3)
-    const int s0e = c * TILE_PIX;
+    const int s0e = (c * TILE_PIX) << d.ck_shift;
     unsigned id_cur = stager && s0e + lane < n ? ids[s0e + lane] : 0u;
     if (stager && s0e + lane < n) stage_dma(S.buf[0], 0, id_cur, (size_t)bv * d.N, b, d.N, gP, gQ, gauss);
     unsigned id_next = stager && s0e + BWD_CHUNK + lane < n ? ids[s0e + BWD_CHUNK + lane] : 0u;
@@ -818,12 +818,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEPTH ? 2 :
     const int4 wl4 = reinterpret_cast<const int4 *>(wlast_fwd)[tile];
     const int wlast = w == 0 ? wl4.x : w == 1 ? wl4.y : w == 2 ? wl4.z : wl4.w;
     const int nlist = min(n, max(max(wl4.x, wl4.y), max(wl4.z, wl4.w)));
-    const int s0 = c * TILE_PIX;
+    const int s0 = (c * TILE_PIX) << d.ck_shift;
     if (s0 >= nlist) {  // workgroup-uniform (the early DMA must land before the workgroup retires)
         vm_wait_all();
         return;
     }
-    const int s1 = (c + 1 <= nck[tile]) ? min(nlist, s0 + TILE_PIX) : nlist;
+    const int s1 = (c + 1 <= nck[tile]) ? min(nlist, s0 + (TILE_PIX << d.ck_shift)) : nlist;
     if (s0 >= s1) {  // (nothing to do; likewise)
         vm_wait_all();
         return;

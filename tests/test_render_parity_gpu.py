@@ -414,6 +414,31 @@ def test_small_launch_form_bitwise(cuda, H, W, N, seed):
     assert torch.allclose(alone[7].cpu(), batched[7].cpu(), rtol=1e-5, atol=0)
 
 
+def test_two_chunk_items_float_path_vs_oracle(cuda, oracle_mod):
+    """Launches of >= CK_LONG_TILES (4,096) tiles split the backward into work items of two forward chunks
+    (render_common.h ck_shift_for; the 8-scene pool takes it). The production float path on such a launch -- the pool's
+    scene 0 repeated three times, 4,608 tiles -- against the oracle for every copy (deterministic mode, which has no
+    checkpoint items, cannot cover it)."""
+    B, N, V, R = 3, 100_000, 6, 256
+    g0 = synthetic_gaussians(1, N, seed=2)
+    cv, cvp, _ = orbit_cameras(V)
+    c0, cp0 = cv[None], cvp[None]
+    d_img, _, d_alpha, bg = synthetic_upstream_grads(1, V, R, R, seed=1002)
+    assert B * V * (R // 16) ** 2 >= 4096
+    d_m, keep = _clamp_masked_grads(oracle_mod, g0, c0, cp0, R, R, bg, d_img)
+
+    def rep(t):
+        return t.expand(B, *t.shape[1:]).contiguous()
+
+    out = _production(cuda, rep(g0), rep(c0), rep(cp0), R, R, bg, rep(d_img), rep(d_alpha), rep(keep))
+    _check(oracle_mod, {k: v[0:1] for k, v in out.items()}, g0, c0, cp0, R, R, bg, d_m, d_alpha,
+           name="two-chunk items, copy 0")
+    for s in range(1, B):  # the other copies: the same forward bit for bit, the float-atomic gradients within 1e-5
+        assert np.array_equal(out["image"][s], out["image"][0]) and np.array_equal(out["alpha"][s], out["alpha"][0])
+        e = rel_l2(out["d_gaussians"][s], out["d_gaussians"][0])
+        assert e < 1e-5, f"copy {s}: gradient rel L2 {e:.3e} vs copy 0"
+
+
 def test_deterministic_checkpoint_split_independent_of_batch(cuda):
     """Deterministic mode on a scene whose tiles walk many chunks (72^2, long lists: the shared checkpoint pool
     would run out): the split of each tile's walk into backward work items follows the tile's own checkpoint quota,

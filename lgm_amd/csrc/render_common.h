@@ -79,7 +79,10 @@ struct Layout {
 // (each workgroup hand-over idles a slot for a few us); one for smaller launches, whose head items already exceed
 // one residency round. Pool (12,288 tiles): k_render_bwd 599 -> 588 us and k_render_fwd -6 us (fewer checkpoints);
 // one cfg3 scene (1,536 tiles) with 2: bwd 92.7 -> 102.8 us (profiles/r06/ab_bwd_cks).
-constexpr size_t CK_LONG_TILES = 4096;
+#ifndef LGM_CK_LONG_TILES
+#define LGM_CK_LONG_TILES 4096
+#endif
+constexpr size_t CK_LONG_TILES = LGM_CK_LONG_TILES;
 #ifdef LGM_CK_SHIFT0  // (A/B: one chunk per item at every size)
 __host__ __device__ __forceinline__ int ck_shift_for(size_t) { return 0; }
 #else
